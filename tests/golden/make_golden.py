@@ -1,0 +1,115 @@
+"""Generate the committed golden vectors from the independent big-int model.
+
+    python tests/golden/make_golden.py
+
+Every fixture is (inputs, expected outputs) computed by
+oracle/bigint_model.py with Python integers.  They pin the C oracle
+(tests/test_oracle_golden.py) and the HIP backend (tests/test_gpu_parity.py).
+No reference code is involved: herdsman has no FHE arithmetic to run
+(SURVEY.md §0), so parity vs herdsman/OpenFHE is "unpinned" and these vectors
+pin the implementation to the mathematical definitions instead.
+"""
+from __future__ import annotations
+
+import os
+import random
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+import bigint_model as M  # noqa: E402
+
+
+def rand_limbs(rng, mods, n):
+    return [[rng.randrange(q) for _ in range(n)] for q in mods]
+
+
+def arr(x):
+    return np.array(x, dtype=np.uint64)
+
+
+def gen_ntt(rng):
+    log_n = 10
+    n = 1 << log_n
+    mods = M.gen_primes(60, log_n, 3)
+    p = M.Params(log_n, 3, 0, 1, mods)
+    x = rand_limbs(rng, mods, n)
+    y = p.ntt(x, range(3))
+    # the fast model NTT must agree with the O(N^2) definition
+    small = M.Params(6, 1, 0, 1, M.gen_primes(60, 6, 1))
+    xs = [rng.randrange(small.moduli[0]) for _ in range(64)]
+    assert M.ntt_fwd(xs, small.moduli[0], small.psi[0]) == M.ntt_fwd_direct(xs, small.moduli[0], small.psi[0])
+    assert p.intt(y, range(3)) == x
+    # negacyclic product theorem
+    a, b = x[0], x[1][:]
+    q = mods[0]
+    lhs = M.ntt_inv([u * v % q for u, v in zip(M.ntt_fwd(a, q, p.psi[0]), M.ntt_fwd(b, q, p.psi[0]))], q, p.psi[0])
+    assert lhs == M.negacyclic_mul(a, b, q)
+    np.savez(os.path.join(HERE, "ntt_n1024.npz"), log_n=np.uint32(log_n), moduli=arr(mods),
+             psi=arr(p.psi), x=arr(x), y=arr(y))
+
+
+def gen_conv(rng):
+    log_n = 8
+    n = 1 << log_n
+    mods = M.gen_primes(60, log_n, 4) + M.gen_primes(61, log_n, 3)
+    src, dst = [0, 1, 2, 3], [4, 5, 6]
+    x = rand_limbs(rng, [mods[i] for i in src], n)
+    y = M.base_conv(x, [mods[i] for i in src], [mods[i] for i in dst])
+    np.savez(os.path.join(HERE, "conv_n256.npz"), log_n=np.uint32(log_n), moduli=arr(mods),
+             src=np.array(src, dtype=np.uint32), dst=np.array(dst, dtype=np.uint32), x=arr(x), y=arr(y))
+
+
+def gen_ckks(rng):
+    log_n, L, K, dnum = 10, 4, 2, 2
+    n = 1 << log_n
+    Q = M.gen_primes(60, log_n, L)
+    P = M.gen_primes(61, log_n, K, exclude=Q)
+    p = M.Params(log_n, L, K, dnum, Q + P, "ckks")
+    a = [rand_limbs(rng, Q, n) for _ in range(2)]
+    b = [rand_limbs(rng, Q, n) for _ in range(2)]
+    rlk = [[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(dnum)]
+    gk = [[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(dnum)]
+    out_mul = M.ckks_mul_relin(p, a, b, rlk)
+    g = M.galois_elt(log_n, 3)
+    out_rot = M.rotate(p, a, g, gk)
+    g_conj = 2 * n - 1
+    out_conj = M.rotate(p, b, g_conj, gk)
+    np.savez(os.path.join(HERE, "ckks_n1024_l4.npz"), log_n=np.uint32(log_n), L=np.uint32(L), K=np.uint32(K),
+             dnum=np.uint32(dnum), moduli=arr(Q + P), a=arr(a), b=arr(b), rlk=arr(rlk), gk=arr(gk),
+             out_mul=arr(out_mul), g=np.uint32(g), out_rot=arr(out_rot), g_conj=np.uint32(g_conj),
+             out_conj=arr(out_conj))
+
+
+def gen_bfv(rng):
+    log_n, L, K, dnum, t = 10, 4, 2, 2, 65537
+    n = 1 << log_n
+    Q = M.gen_primes(60, log_n, L)
+    P = M.gen_primes(61, log_n, K, exclude=Q)
+    Bsk = M.gen_primes(61, log_n, L + 1, exclude=Q + P)
+    p = M.Params(log_n, L, K, dnum, Q + P + Bsk, "bfv", t)
+    a = [rand_limbs(rng, Q, n) for _ in range(2)]
+    b = [rand_limbs(rng, Q, n) for _ in range(2)]
+    rlk = [[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(dnum)]
+    out_mul = M.bfv_mul_relin(p, a, b, rlk)
+    out_add = [[[(x + y) % Q[i] for x, y in zip(a[c][i], b[c][i])] for i in range(L)] for c in range(2)]
+    g = M.galois_elt(log_n, 1)
+    out_rot = M.rotate(p, a, g, rlk)
+    np.savez(os.path.join(HERE, "bfv_n1024_l4.npz"), log_n=np.uint32(log_n), L=np.uint32(L), K=np.uint32(K),
+             dnum=np.uint32(dnum), t=np.uint64(t), moduli=arr(Q + P + Bsk), a=arr(a), b=arr(b), rlk=arr(rlk),
+             out_mul=arr(out_mul), out_add=arr(out_add), g=np.uint32(g), out_rot=arr(out_rot))
+
+
+def main():
+    rng = random.Random(0x48455244)
+    gen_ntt(rng)
+    gen_conv(rng)
+    gen_ckks(rng)
+    gen_bfv(rng)
+    print("golden vectors written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

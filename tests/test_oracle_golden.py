@@ -1,0 +1,85 @@
+"""The C oracle (oracle/fhe_oracle.c) against the big-int golden vectors.
+
+This is what pins the oracle before it is trusted as the checker for the HIP
+backend (tests/test_gpu_parity.py).  Fixtures: tests/golden/*.npz, produced by
+tests/golden/make_golden.py from oracle/bigint_model.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle_ffi import Oracle, SCHEME_BFV, SCHEME_CKKS
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+def test_prime_generation_matches_model():
+    g = load("ckks_n1024_l4.npz")
+    o = Oracle(SCHEME_CKKS, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]))
+    assert np.array_equal(o.moduli, g["moduli"])
+
+
+def test_ntt_golden():
+    g = load("ntt_n1024.npz")
+    o = Oracle(SCHEME_CKKS, int(g["log_n"]), 3, moduli=g["moduli"])
+    for i in range(3):
+        assert o.lib.orc_psi(o.h, i) == int(g["psi"][i])
+    y = o.ntt_fwd(g["x"])
+    assert np.array_equal(y, g["y"])
+    assert np.array_equal(o.ntt_inv(y), g["x"])
+
+
+def test_base_conv_golden():
+    g = load("conv_n256.npz")
+    o = Oracle(SCHEME_CKKS, int(g["log_n"]), len(g["moduli"]), moduli=g["moduli"])
+    y = o.base_conv(g["x"], g["src"], g["dst"])
+    assert np.array_equal(y[0], g["y"])
+
+
+def _ckks():
+    g = load("ckks_n1024_l4.npz")
+    o = Oracle(SCHEME_CKKS, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), moduli=g["moduli"])
+    return g, o
+
+
+def test_ckks_mul_relin_golden():
+    g, o = _ckks()
+    out = o.mul_relin(g["a"][None], g["b"][None], g["rlk"])
+    assert np.array_equal(out[0], g["out_mul"])
+
+
+def test_ckks_rotate_golden():
+    g, o = _ckks()
+    out = o.rotate(g["a"][None], int(g["g"]), g["gk"])
+    assert np.array_equal(out[0], g["out_rot"])
+    out = o.rotate(g["b"][None], int(g["g_conj"]), g["gk"])
+    assert np.array_equal(out[0], g["out_conj"])
+
+
+def _bfv():
+    g = load("bfv_n1024_l4.npz")
+    o = Oracle(SCHEME_BFV, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), t=int(g["t"]),
+               moduli=g["moduli"])
+    return g, o
+
+
+def test_bfv_add_golden():
+    g, o = _bfv()
+    assert np.array_equal(o.ct_add(g["a"][None], g["b"][None])[0], g["out_add"])
+
+
+def test_bfv_mul_relin_golden():
+    g, o = _bfv()
+    out = o.mul_relin(g["a"][None], g["b"][None], g["rlk"])
+    assert np.array_equal(out[0], g["out_mul"])
+
+
+def test_bfv_rotate_golden():
+    g, o = _bfv()
+    out = o.rotate(g["a"][None], int(g["g"]), g["rlk"])
+    assert np.array_equal(out[0], g["out_rot"])

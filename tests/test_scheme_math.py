@@ -1,0 +1,95 @@
+"""Scheme-level ground truth for the oracle with REAL keys.
+
+Decrypt(MulRelin(Enc(m1), Enc(m2))) and Decrypt(Rotate(Enc(m))) are checked
+with exact CRT reconstruction against the integer negacyclic product /
+automorphism.  These identities pin the key-switching
+algorithm itself, independently of any golden vector.
+"""
+import math
+import random
+
+import numpy as np
+
+from fhe_math import automorph_int, crt_centered, negacyclic_int, to_rns
+from oracle_ffi import Oracle, SCHEME_BFV, SCHEME_CKKS
+
+
+def _keys(o, seed=11):
+    s = o.secret(seed)
+    s_qp = o.signed_to_rns(s, 0, o.L + o.K, ntt=True)
+    return s, s_qp
+
+
+def _square_ntt(o, s_qp):
+    out = np.zeros_like(s_qp)
+    for i in range(o.L + o.K):
+        q = int(o.moduli[i])
+        out[i] = np.array([(int(x) * int(x)) % q for x in s_qp[i]], dtype=np.uint64)
+    return out
+
+
+def test_ckks_mul_relin_decrypts():
+    o = Oracle(SCHEME_CKKS, 10, 4, 2, 2)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    s, s_qp = _keys(o)
+    rlk = o.switch_key(_square_ntt(o, s_qp), s_qp, seed=5)
+    rng = random.Random(1)
+    delta = 1 << 30
+    u1 = [rng.randint(-8, 8) for _ in range(o.n)]
+    u2 = [rng.randint(-8, 8) for _ in range(o.n)]
+    c1 = o.encrypt(to_rns([delta * x for x in u1], Q), s_qp, 101)
+    c2 = o.encrypt(to_rns([delta * x for x in u2], Q), s_qp, 202)
+    prod = o.mul_relin(c1[None], c2[None], rlk)[0]
+    dec = crt_centered(o.decrypt(prod, s_qp), Q)
+    want = [delta * delta * v for v in negacyclic_int(u1, u2)]
+    err = max(abs(a - b) for a, b in zip(dec, want))
+    assert err < 2 ** 56, math.log2(err + 1)
+
+
+def test_ckks_rotate_decrypts():
+    o = Oracle(SCHEME_CKKS, 10, 4, 2, 2)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    s, s_qp = _keys(o)
+    rng = random.Random(2)
+    delta = 1 << 40
+    u = [rng.randint(-100, 100) for _ in range(o.n)]
+    ct = o.encrypt(to_rns([delta * x for x in u], Q), s_qp, 303)
+    for steps in (1, 5, -3):
+        g = o.galois_elt(steps)
+        s_g = o.automorph_ntt(s_qp, g)
+        gk = o.switch_key(s_g, s_qp, seed=9 + steps)
+        rot = o.rotate(ct[None], g, gk)[0]
+        dec = crt_centered(o.decrypt(rot, s_qp), Q)
+        want = [delta * v for v in automorph_int(u, g)]
+        err = max(abs(a - b) for a, b in zip(dec, want))
+        assert err < 2 ** 30, (steps, math.log2(err + 1))
+
+
+def test_bfv_mul_relin_decrypts_exactly():
+    t = 65537
+    o = Oracle(SCHEME_BFV, 10, 4, 2, 2, t=t)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    Qp = math.prod(Q)
+    s, s_qp = _keys(o)
+    rlk = o.switch_key(_square_ntt(o, s_qp), s_qp, seed=6)
+    rng = random.Random(3)
+    delta = Qp // t
+    m1 = [rng.randrange(t) for _ in range(o.n)]
+    m2 = [rng.randrange(t) for _ in range(o.n)]
+    c1 = o.encrypt(to_rns([delta * x for x in m1], Q), s_qp, 404)
+    c2 = o.encrypt(to_rns([delta * x for x in m2], Q), s_qp, 505)
+
+    def dec(ct):
+        v = crt_centered(o.decrypt(ct, s_qp), Q)
+        return [((t * x + Qp // 2) // Qp) % t for x in v]
+
+    assert dec(c1) == m1
+    prod = o.mul_relin(c1[None], c2[None], rlk)[0]
+    want = [v % t for v in negacyclic_int(m1, m2)]
+    assert dec(prod) == want
+    add = o.ct_add(c1[None], c2[None])[0]
+    assert dec(add) == [(a + b) % t for a, b in zip(m1, m2)]
+    g = o.galois_elt(1)
+    gk = o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=8)
+    rot = o.rotate(c1[None], g, gk)[0]
+    assert dec(rot) == [v % t for v in automorph_int(m1, g)]
