@@ -1,0 +1,253 @@
+"""ctypes binding of libherdsman_fhe.so (include/plugins/fhe_backend.h).
+
+Device buffers are torch tensors on a HIP device (PyTorch is only the
+allocator/stream provider here); their data pointers go straight to the C ABI.
+There is NO CPU fallback: if the library is missing or no GPU is present every
+call raises FheBackendError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SCHEME_CKKS = 0
+SCHEME_BFV = 1
+
+FHE_OK = 0
+_ERRORS = {-1: "FHE_ERR_INVALID", -2: "FHE_ERR_DEVICE", -3: "FHE_ERR_OOM", -4: "FHE_ERR_UNSUPPORTED"}
+
+
+class FheBackendError(RuntimeError):
+    pass
+
+
+class _Params(C.Structure):
+    _fields_ = [
+        ("scheme", C.c_uint32),
+        ("log_n", C.c_uint32),
+        ("num_q", C.c_uint32),
+        ("num_p", C.c_uint32),
+        ("dnum", C.c_uint32),
+        ("q_bits", C.c_uint32),
+        ("p_bits", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("plain_modulus", C.c_uint64),
+        ("moduli", C.c_void_p),
+    ]
+
+
+# name -> (restype, argtypes); also the list of exported symbols the CPU
+# tests check against include/plugins/fhe_backend.h
+_vp, _u32, _u64, _i32, _sz = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32, C.c_size_t
+SIGNATURES = {
+    "fhe_ctx_create": (C.c_int, [C.POINTER(_Params), C.c_int, C.POINTER(_vp)]),
+    "fhe_ctx_destroy": (None, [_vp]),
+    "fhe_last_error": (C.c_char_p, [_vp]),
+    "fhe_ctx_moduli": (C.c_int, [_vp, _vp, _u32, C.POINTER(_u32)]),
+    "fhe_set_stream": (C.c_int, [_vp, _vp]),
+    "fhe_synchronize": (C.c_int, [_vp]),
+    "fhe_reserve": (C.c_int, [_vp, _u32]),
+    "fhe_dev_alloc": (C.c_int, [_vp, _sz, C.POINTER(_vp)]),
+    "fhe_dev_free": (C.c_int, [_vp, _vp]),
+    "fhe_memcpy_h2d": (C.c_int, [_vp, _vp, _vp, _sz]),
+    "fhe_memcpy_d2h": (C.c_int, [_vp, _vp, _vp, _sz]),
+    "fhe_ntt_fwd": (C.c_int, [_vp, _vp, _u32, _u32, _u32]),
+    "fhe_ntt_inv": (C.c_int, [_vp, _vp, _u32, _u32, _u32]),
+    "fhe_poly_add": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32, _u32]),
+    "fhe_poly_sub": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32, _u32]),
+    "fhe_poly_mul": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32, _u32]),
+    "fhe_base_conv": (C.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _u32, _u32]),
+    "fhe_fill_uniform": (C.c_int, [_vp, _vp, _u32, _u32, _u32, _u64]),
+    "fhe_add": (C.c_int, [_vp, _vp, _vp, _vp, _u32]),
+    "fhe_sub": (C.c_int, [_vp, _vp, _vp, _vp, _u32]),
+    "fhe_mul_relin": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _u32]),
+    "fhe_keyswitch": (C.c_int, [_vp, _vp, _vp, _vp, _u32]),
+    "fhe_rotate": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _u32]),
+    "fhe_galois_elt": (C.c_int, [_vp, _i32, C.POINTER(_u32)]),
+    "fhe_bcast_key": (C.c_int, [_vp, _vp, _sz, _vp, C.c_int]),
+}
+
+_lib = None
+
+
+def library_path() -> str:
+    return os.path.join(HERE, "lib", "libherdsman_fhe.so")
+
+
+def load_library():
+    """Load the HIP backend; raises (never falls back) when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not os.path.exists(path):
+        raise FheBackendError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    _lib = lib
+    return lib
+
+
+def _ptr(t) -> int:
+    """Device pointer of a torch tensor (must be contiguous, on a HIP device)."""
+    if not t.is_cuda:
+        raise FheBackendError("buffer must live on the GPU (torch tensor on a HIP device)")
+    if not t.is_contiguous():
+        raise FheBackendError("buffer must be contiguous")
+    if t.element_size() != 8:
+        raise FheBackendError("buffer must hold 64-bit words")
+    return t.data_ptr()
+
+
+class Context:
+    """One device context (params + twiddle/CRT tables + workspace)."""
+
+    def __init__(self, scheme: int, log_n: int, L: int, K: int = 0, dnum: int = 1, q_bits: int = 60,
+                 p_bits: int = 61, t: int = 0, moduli: Optional[Sequence[int]] = None, device: int = 0):
+        self.lib = load_library()
+        self.scheme, self.log_n, self.n = scheme, log_n, 1 << log_n
+        self.L, self.K, self.dnum, self.t = L, K, dnum, t
+        self.alpha = -(-L // dnum)
+        self._mods_keep = None
+        mp = None
+        if moduli is not None:
+            self._mods_keep = np.ascontiguousarray(np.asarray(moduli, dtype=np.uint64))
+            mp = self._mods_keep.ctypes.data
+        p = _Params(scheme, log_n, L, K, dnum, q_bits, p_bits, 0, t, mp)
+        h = C.c_void_p()
+        rc = self.lib.fhe_ctx_create(C.byref(p), device, C.byref(h))
+        if rc != FHE_OK:
+            msg = self.lib.fhe_last_error(None)
+            raise FheBackendError(f"fhe_ctx_create: {_ERRORS.get(rc, rc)}: {msg.decode() if msg else ''}")
+        self.h = h
+        cnt = _u32()
+        self.lib.fhe_ctx_moduli(self.h, None, 0, C.byref(cnt))
+        self.moduli = np.zeros(cnt.value, dtype=np.uint64)
+        self.lib.fhe_ctx_moduli(self.h, self.moduli.ctypes.data, cnt.value, None)
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fhe_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ck(self, rc, what):
+        if rc != FHE_OK:
+            msg = self.lib.fhe_last_error(self.h)
+            raise FheBackendError(f"{what}: {_ERRORS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    # ---- streams
+    def set_stream(self, stream):
+        """Enqueue on a torch.cuda.Stream (or raw hipStream_t int)."""
+        raw = stream if isinstance(stream, int) else stream.cuda_stream
+        self._ck(self.lib.fhe_set_stream(self.h, raw), "fhe_set_stream")
+
+    def synchronize(self):
+        self._ck(self.lib.fhe_synchronize(self.h), "fhe_synchronize")
+
+    def reserve(self, max_batch: int):
+        self._ck(self.lib.fhe_reserve(self.h, max_batch), "fhe_reserve")
+
+    # ---- shapes
+    def ct_shape(self, n_ct: int = 1):
+        return (n_ct, 2, self.L, self.n)
+
+    def key_shape(self):
+        return (self.dnum, 2, self.L + self.K, self.n)
+
+    # ---- primitives
+    def _limbs(self, x):
+        nl = x.shape[-2]
+        if x.shape[-1] != self.n:
+            raise FheBackendError(f"last dim must be N={self.n}")
+        return x.numel() // (nl * self.n), nl
+
+    def ntt_fwd(self, x, mod_begin: int = 0):
+        n, nl = self._limbs(x)
+        self._ck(self.lib.fhe_ntt_fwd(self.h, _ptr(x), n, mod_begin, nl), "fhe_ntt_fwd")
+        return x
+
+    def ntt_inv(self, x, mod_begin: int = 0):
+        n, nl = self._limbs(x)
+        self._ck(self.lib.fhe_ntt_inv(self.h, _ptr(x), n, mod_begin, nl), "fhe_ntt_inv")
+        return x
+
+    def poly_op(self, op: str, a, b, out, mod_begin: int = 0):
+        n, nl = self._limbs(a)
+        fn = {"add": self.lib.fhe_poly_add, "sub": self.lib.fhe_poly_sub, "mul": self.lib.fhe_poly_mul}[op]
+        self._ck(fn(self.h, _ptr(a), _ptr(b), _ptr(out), n, mod_begin, nl), f"fhe_poly_{op}")
+        return out
+
+    def base_conv(self, src, src_mods, dst, dst_mods):
+        s = np.ascontiguousarray(src_mods, dtype=np.uint32)
+        d = np.ascontiguousarray(dst_mods, dtype=np.uint32)
+        n = src.numel() // (len(s) * self.n)
+        self._ck(self.lib.fhe_base_conv(self.h, _ptr(src), s.ctypes.data, len(s), _ptr(dst), d.ctypes.data,
+                                        len(d), n), "fhe_base_conv")
+        return dst
+
+    def fill_uniform(self, x, seed: int, mod_begin: int = 0):
+        n, nl = self._limbs(x)
+        self._ck(self.lib.fhe_fill_uniform(self.h, _ptr(x), n, mod_begin, nl, seed & (2**64 - 1)),
+                 "fhe_fill_uniform")
+        return x
+
+    # ---- ciphertext ops
+    def add(self, a, b, out):
+        self._ck(self.lib.fhe_add(self.h, _ptr(a), _ptr(b), _ptr(out), a.shape[0]), "fhe_add")
+        return out
+
+    def sub(self, a, b, out):
+        self._ck(self.lib.fhe_sub(self.h, _ptr(a), _ptr(b), _ptr(out), a.shape[0]), "fhe_sub")
+        return out
+
+    def mul_relin(self, a, b, rlk, out):
+        self._ck(self.lib.fhe_mul_relin(self.h, _ptr(a), _ptr(b), _ptr(rlk), _ptr(out), a.shape[0]),
+                 "fhe_mul_relin")
+        return out
+
+    def keyswitch(self, d, ksk, out):
+        self._ck(self.lib.fhe_keyswitch(self.h, _ptr(d), _ptr(ksk), _ptr(out), d.shape[0]), "fhe_keyswitch")
+        return out
+
+    def rotate(self, ct, galois: int, gk, out):
+        self._ck(self.lib.fhe_rotate(self.h, _ptr(ct), galois, _ptr(gk), _ptr(out), ct.shape[0]), "fhe_rotate")
+        return out
+
+    def galois_elt(self, steps: int) -> int:
+        g = _u32()
+        self._ck(self.lib.fhe_galois_elt(self.h, steps, C.byref(g)), "fhe_galois_elt")
+        return g.value
+
+    def bcast_key(self, key, nccl_comm: int, root: int = 0):
+        self._ck(self.lib.fhe_bcast_key(self.h, _ptr(key), key.numel(), nccl_comm, root), "fhe_bcast_key")
+
+
+# ---- torch <-> numpy helpers (u64 payload in int64 tensors)
+def to_device(arr: np.ndarray, device="cuda"):
+    import torch
+
+    a = np.ascontiguousarray(arr, dtype=np.uint64)
+    return torch.from_numpy(a.view(np.int64)).to(device)
+
+
+def to_host(t) -> np.ndarray:
+    return t.detach().cpu().numpy().view(np.uint64)
+
+
+def empty(shape, device="cuda"):
+    import torch
+
+    return torch.empty(shape, dtype=torch.int64, device=device)

@@ -1,0 +1,92 @@
+// context.hpp -- internal state behind the fhe_ctx handle of fhe_backend.h.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/plugins/fhe_backend.h"
+#include "modarith.hpp"
+
+#define FHE_MAX_MODS 48
+#define FHE_MAX_CONV_SRC 16
+
+// A batch of limb-polynomials inside a [poly][poly_stride][N] buffer: active
+// limb a of poly p is limb `first + (a < skip_lo ? a : a + skip_len)` and uses
+// modulus `mod_offset + limb`.  Covers whole polys, Q- or P-parts and the
+// "all limbs except this digit" sets of ModUp.
+struct LimbMap {
+  u64 *base;
+  u32 poly_stride;
+  u32 cnt;
+  u32 first;
+  u32 skip_lo;
+  u32 skip_len;
+  u32 mod_offset;
+  u32 n_polys;
+};
+
+__host__ __device__ __forceinline__ u32 limbmap_limb(const LimbMap &m, u32 act) {
+  return m.first + (act < m.skip_lo ? act : act + m.skip_len);
+}
+
+// Fast base conversion table (device): src moduli -> dst moduli.
+struct ConvTab {
+  u32 ns, nd;
+  const u32 *src_mod; // [ns] modulus ids of the sources
+  const u32 *dst_mod; // [nd] modulus ids of the destinations
+  const Tw *hinv;     // [ns] {(S/s_i)^-1 mod s_i, Shoup}
+  const u64 *h;       // [ns][nd] (S/s_i) mod d_m
+};
+// host-side construction (ops.cpp); uploads into context-owned device memory
+ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst);
+
+struct BehzTabDev;  // defined in rns.hip
+
+struct fhe_ctx {
+  fhe_params params{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  u32 log_n = 0, n = 0, L = 0, K = 0, dnum = 0, alpha = 0, nB = 0, nmod = 0;
+  u64 t = 0;
+  std::vector<u64> moduli;
+  // device-resident tables
+  ModInfo *d_mods = nullptr;   // [nmod]
+  Tw *d_tw_fwd = nullptr;      // [nmod][N]  psi^brv(i)
+  Tw *d_tw_inv = nullptr;      // [nmod][N]  psi^-brv(i)
+  Tw *d_ninv = nullptr;        // [nmod]     N^-1
+  Tw *d_pinv = nullptr;        // [L]        P^-1 mod q_i
+  // ModUp tables per digit, ModDown table (device blobs + host descriptors)
+  ConvTab *d_modup = nullptr;  // device array [dnum]
+  ConvTab moddown{};
+  std::vector<void *> blobs;   // device allocations owned by the context
+  void *behz = nullptr;        // BEHZ device constants (BFV)
+  // scratch
+  void *ws = nullptr;
+  size_t ws_bytes = 0;
+};
+
+// helpers shared by the translation units
+int fhe_fail(fhe_ctx *c, int code, const std::string &msg);
+int fhe_check(fhe_ctx *c, hipError_t e, const char *what);
+void *ctx_upload(fhe_ctx *c, const void *host, size_t bytes);  // owned blob
+int ctx_workspace(fhe_ctx *c, size_t bytes, void **out);
+
+// NTT (ntt.hip)
+int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse);
+// RNS kernels (rns.hip)
+enum class EwOp { Add, Sub, Mul };
+int ew_launch(fhe_ctx *c, EwOp op, const u64 *a, const u64 *b, u64 *out, u32 n_polys, u32 mod_begin, u32 n_limbs);
+int conv_launch(fhe_ctx *c, const ConvTab &t, const u64 *src, u32 src_poly_stride, u64 *dst,
+                u32 dst_poly_stride, u32 n);
+int fill_uniform_launch(fhe_ctx *c, u64 *data, u32 n_polys, u32 mod_begin, u32 n_limbs, u64 seed);
+int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u64 *base, u64 *out, u32 n,
+                 u32 add_mask, bool ntt_form, u64 *ws);
+int tensor_launch(fhe_ctx *c, const u64 *a, size_t a_ct, size_t a_poly, const u64 *b, size_t b_ct, size_t b_poly,
+                  u64 *e01, size_t e_ct, size_t e_poly, u64 *e2, size_t e2_ct, u32 n_ct, u32 nl, u32 mod_offset);
+int automorph_launch(fhe_ctx *c, const u64 *in, u64 *out, u32 g, u32 n_polys, bool ntt_form);
+int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n_ct);
+int behz_setup(fhe_ctx *c);
+size_t keyswitch_ws_bytes(const fhe_ctx *c, u32 n);
+size_t bfv_mul_ws_bytes(const fhe_ctx *c, u32 n);

@@ -1,0 +1,475 @@
+// fhe_backend.cpp -- C ABI (include/plugins/fhe_backend.h): context setup,
+// parameter precomputation and op orchestration.  Host code only; kernels
+// live in ntt.hip / rns.hip.  Nothing here computes on the CPU what the ABI
+// promises to compute on the GPU: host work is limited to one-off table
+// generation at context creation (primes, roots, CRT constants).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "context.hpp"
+
+typedef unsigned __int128 u128;
+
+// ------------------------------------------------------------ host math
+static u64 hmul(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
+static u64 hpow(u64 b, u64 e, u64 q) {
+  u64 r = 1 % q;
+  b %= q;
+  while (e) {
+    if (e & 1) r = hmul(r, b, q);
+    b = hmul(b, b, q);
+    e >>= 1;
+  }
+  return r;
+}
+static u64 hinv(u64 a, u64 q) { return hpow(a % q, q - 2, q); }
+static Tw htw(u64 w, u64 q) { return Tw{w, (u64)(((u128)w << 64) / q)}; }
+static u32 hbrv(u32 x, u32 bits) {
+  u32 r = 0;
+  for (u32 i = 0; i < bits; ++i) { r = (r << 1) | (x & 1); x >>= 1; }
+  return r;
+}
+static bool is_prime(u64 n) {
+  static const u64 bases[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+  if (n < 2) return false;
+  for (u64 b : bases) {
+    if (n == b) return true;
+    if (n % b == 0) return false;
+  }
+  u64 d = n - 1;
+  int s = 0;
+  while (!(d & 1)) { d >>= 1; ++s; }
+  for (u64 a : bases) {
+    u64 x = hpow(a, d, n);
+    if (x == 1 || x == n - 1) continue;
+    bool comp = true;
+    for (int r = 1; r < s; ++r) {
+      x = hmul(x, x, n);
+      if (x == n - 1) { comp = false; break; }
+    }
+    if (comp) return false;
+  }
+  return true;
+}
+// largest primes q < 2^bits, q = 1 mod 2N, descending, not in `used`
+static bool gen_primes(u32 bits, u32 log_n, u32 count, std::vector<u64> &used, std::vector<u64> &out) {
+  const u64 two_n = 2ull << log_n;
+  for (u64 k = ((1ull << bits) - 2) / two_n; k > 0 && count; --k) {
+    const u64 q = k * two_n + 1;
+    if (std::find(used.begin(), used.end(), q) != used.end()) continue;
+    if (is_prime(q)) { out.push_back(q); used.push_back(q); --count; }
+  }
+  return count == 0;
+}
+// smallest primitive 2N-th root of unity mod q
+static u64 min_psi(u64 q, u32 log_n) {
+  const u64 n = 1ull << log_n;
+  u64 g = 0;
+  for (u64 x = 2; x < q; ++x) {
+    g = hpow(x, (q - 1) / (2 * n), q);
+    if (hpow(g, n, q) == q - 1) break;
+  }
+  const u64 g2 = hmul(g, g, q);
+  u64 best = g, cur = g;
+  for (u64 k = 1; k < n; ++k) {
+    cur = hmul(cur, g2, q);
+    if (cur < best) best = cur;
+  }
+  return best;
+}
+
+// ------------------------------------------------------------ helpers
+int fhe_fail(fhe_ctx *c, int code, const std::string &msg) {
+  if (c) c->err = msg;
+  return code;
+}
+int fhe_check(fhe_ctx *c, hipError_t e, const char *what) {
+  if (e == hipSuccess) return FHE_OK;
+  return fhe_fail(c, e == hipErrorOutOfMemory ? FHE_ERR_OOM : FHE_ERR_DEVICE,
+                  std::string(what) + ": " + hipGetErrorString(e));
+}
+void *ctx_upload(fhe_ctx *c, const void *host, size_t bytes) {
+  void *p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  if (hipMemcpy(p, host, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  c->blobs.push_back(p);
+  return p;
+}
+int ctx_workspace(fhe_ctx *c, size_t bytes, void **out) {
+  if (bytes > c->ws_bytes) {
+    if (c->ws) {
+      int rc = fhe_check(c, hipStreamSynchronize(c->stream), "workspace sync");
+      if (rc) return rc;
+      (void)hipFree(c->ws);
+      c->ws = nullptr;
+      c->ws_bytes = 0;
+    }
+    int rc = fhe_check(c, hipMalloc(&c->ws, bytes), "workspace alloc");
+    if (rc) return rc;
+    c->ws_bytes = bytes;
+  }
+  *out = c->ws;
+  return FHE_OK;
+}
+
+ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst) {
+  ConvTab t{};
+  t.ns = (u32)src.size();
+  t.nd = (u32)dst.size();
+  std::vector<Tw> hi(t.ns);
+  std::vector<u64> h((size_t)t.ns * t.nd);
+  for (u32 i = 0; i < t.ns; ++i) {
+    const u64 si = c->moduli[src[i]];
+    u64 prod = 1;
+    for (u32 k = 0; k < t.ns; ++k)
+      if (k != i) prod = hmul(prod, c->moduli[src[k]] % si, si);
+    hi[i] = htw(hinv(prod, si), si);
+    for (u32 m = 0; m < t.nd; ++m) {
+      const u64 dm = c->moduli[dst[m]];
+      u64 p2 = 1;
+      for (u32 k = 0; k < t.ns; ++k)
+        if (k != i) p2 = hmul(p2, c->moduli[src[k]] % dm, dm);
+      h[(size_t)i * t.nd + m] = p2;
+    }
+  }
+  t.src_mod = (const u32 *)ctx_upload(c, src.data(), sizeof(u32) * t.ns);
+  t.dst_mod = (const u32 *)ctx_upload(c, dst.data(), sizeof(u32) * std::max<u32>(t.nd, 1));
+  t.hinv = (const Tw *)ctx_upload(c, hi.data(), sizeof(Tw) * t.ns);
+  t.h = (const u64 *)ctx_upload(c, h.data(), sizeof(u64) * std::max<size_t>(h.size(), 1));
+  return t;
+}
+
+static void ctx_release(fhe_ctx *c) {
+  if (!c) return;
+  for (void *p : c->blobs) (void)hipFree(p);
+  c->blobs.clear();
+  if (c->ws) (void)hipFree(c->ws);
+  c->ws = nullptr;
+}
+
+// ------------------------------------------------------------ context
+static int ctx_build(fhe_ctx *c, const fhe_params *p) {
+  c->params = *p;
+  c->params.moduli = nullptr;
+  c->log_n = p->log_n;
+  c->n = 1u << p->log_n;
+  c->L = p->num_q;
+  c->K = p->num_p;
+  c->dnum = p->dnum;
+  c->alpha = (c->L + c->dnum - 1) / c->dnum;
+  c->t = p->plain_modulus;
+  c->nB = p->scheme == FHE_SCHEME_BFV ? c->L + 1 : 0;
+  c->nmod = c->L + c->K + c->nB;
+  if (p->scheme > FHE_SCHEME_BFV) return fhe_fail(c, FHE_ERR_INVALID, "unknown scheme");
+  if (p->log_n < 10 || p->log_n > 17) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "log_n must be in [10, 17]");
+  if (c->L == 0 || c->dnum == 0 || c->dnum > c->L) return fhe_fail(c, FHE_ERR_INVALID, "need 1 <= dnum <= L");
+  if (c->alpha > 16) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "alpha = ceil(L/dnum) must be <= 16");
+  if (c->K > 16) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "K must be <= 16");
+  if (c->nmod > FHE_MAX_MODS) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "too many moduli");
+  if (p->scheme == FHE_SCHEME_BFV && (c->t < 2 || c->K == 0))
+    return fhe_fail(c, FHE_ERR_INVALID, "BFV needs a plain modulus t >= 2 and K >= 1");
+  // moduli
+  if (p->moduli) {
+    c->moduli.assign(p->moduli, p->moduli + c->nmod);
+    const u64 two_n = 2ull << p->log_n;
+    for (u64 q : c->moduli)
+      if (q >= (1ull << 62) || q % two_n != 1 || !is_prime(q))
+        return fhe_fail(c, FHE_ERR_INVALID, "explicit modulus is not an NTT-friendly prime < 2^62");
+  } else {
+    if (p->q_bits < 20 || p->q_bits > 61 || p->p_bits < 20 || p->p_bits > 61)
+      return fhe_fail(c, FHE_ERR_INVALID, "q_bits / p_bits must be in [20, 61]");
+    std::vector<u64> used;
+    if (!gen_primes(p->q_bits, p->log_n, c->L, used, c->moduli) ||
+        !gen_primes(p->p_bits, p->log_n, c->K, used, c->moduli) ||
+        !gen_primes(p->p_bits, p->log_n, c->nB, used, c->moduli))
+      return fhe_fail(c, FHE_ERR_INVALID, "not enough NTT-friendly primes");
+  }
+  const u32 n = c->n, nm = c->nmod;
+  // per-modulus tables
+  std::vector<ModInfo> mods(nm);
+  std::vector<Tw> twf((size_t)nm * n), twi((size_t)nm * n), ninv(nm);
+  std::vector<u64> pw(n), ipw(n);
+  for (u32 m = 0; m < nm; ++m) {
+    const u64 q = c->moduli[m];
+    const u128 mu = (~(u128)0) / q;
+    mods[m] = ModInfo{q, (u64)(mu >> 64), (u64)mu, 0};
+    const u64 psi = min_psi(q, c->log_n), ipsi = hinv(psi, q);
+    u64 a = 1, b = 1;
+    for (u32 i = 0; i < n; ++i) { pw[i] = a; ipw[i] = b; a = hmul(a, psi, q); b = hmul(b, ipsi, q); }
+    for (u32 i = 0; i < n; ++i) {
+      const u32 r = hbrv(i, c->log_n);
+      twf[(size_t)m * n + i] = htw(pw[r], q);
+      twi[(size_t)m * n + i] = htw(ipw[r], q);
+    }
+    ninv[m] = htw(hinv(n, q), q);
+  }
+  c->d_mods = (ModInfo *)ctx_upload(c, mods.data(), sizeof(ModInfo) * nm);
+  c->d_tw_fwd = (Tw *)ctx_upload(c, twf.data(), sizeof(Tw) * twf.size());
+  c->d_tw_inv = (Tw *)ctx_upload(c, twi.data(), sizeof(Tw) * twi.size());
+  c->d_ninv = (Tw *)ctx_upload(c, ninv.data(), sizeof(Tw) * nm);
+  if (!c->d_mods || !c->d_tw_fwd || !c->d_tw_inv || !c->d_ninv) return fhe_fail(c, FHE_ERR_OOM, "table upload");
+  // key-switching tables
+  if (c->K) {
+    const u32 L = c->L, QP = c->L + c->K;
+    std::vector<Tw> pinv(L);
+    for (u32 i = 0; i < L; ++i) {
+      const u64 q = c->moduli[i];
+      u64 P = 1;
+      for (u32 k = 0; k < c->K; ++k) P = hmul(P, c->moduli[L + k] % q, q);
+      pinv[i] = htw(hinv(P, q), q);
+    }
+    c->d_pinv = (Tw *)ctx_upload(c, pinv.data(), sizeof(Tw) * L);
+    std::vector<ConvTab> tabs;
+    for (u32 j = 0; j * c->alpha < L; ++j) {
+      const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
+      std::vector<u32> src, dst;
+      for (u32 i = lo; i < hi; ++i) src.push_back(i);
+      for (u32 i = 0; i < QP; ++i)
+        if (i < lo || i >= hi) dst.push_back(i);
+      tabs.push_back(make_conv_tab(c, src, dst));
+    }
+    c->d_modup = (ConvTab *)ctx_upload(c, tabs.data(), sizeof(ConvTab) * tabs.size());
+    std::vector<u32> src, dst;
+    for (u32 k = 0; k < c->K; ++k) src.push_back(L + k);
+    for (u32 i = 0; i < L; ++i) dst.push_back(i);
+    c->moddown = make_conv_tab(c, src, dst);
+    if (!c->d_pinv || !c->d_modup || !c->moddown.h) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
+  }
+  if (p->scheme == FHE_SCHEME_BFV) {
+    int rc = behz_setup(c);
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
+static thread_local std::string g_create_error;
+
+extern "C" {
+
+int fhe_ctx_create(const fhe_params *params, int device, fhe_ctx **out) {
+  if (!params || !out) return FHE_ERR_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    g_create_error = "no HIP device";
+    return FHE_ERR_DEVICE;
+  }
+  if (device < 0 || device >= ndev) return FHE_ERR_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return FHE_ERR_DEVICE;
+  fhe_ctx *c = new (std::nothrow) fhe_ctx();
+  if (!c) return FHE_ERR_OOM;
+  c->device = device;
+  int rc = ctx_build(c, params);
+  if (rc) {
+    g_create_error = c->err;
+    ctx_release(c);
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return FHE_OK;
+}
+
+void fhe_ctx_destroy(fhe_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  ctx_release(c);
+  delete c;
+}
+
+const char *fhe_last_error(const fhe_ctx *c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+
+int fhe_ctx_moduli(const fhe_ctx *c, uint64_t *out, uint32_t cap, uint32_t *count) {
+  if (!c) return FHE_ERR_INVALID;
+  if (count) *count = c->nmod;
+  if (out) std::memcpy(out, c->moduli.data(), sizeof(u64) * std::min(cap, c->nmod));
+  return FHE_OK;
+}
+
+int fhe_set_stream(fhe_ctx *c, void *stream) {
+  if (!c) return FHE_ERR_INVALID;
+  c->stream = (hipStream_t)stream;
+  return FHE_OK;
+}
+
+int fhe_synchronize(fhe_ctx *c) {
+  if (!c) return FHE_ERR_INVALID;
+  return fhe_check(c, hipStreamSynchronize(c->stream), "synchronize");
+}
+
+int fhe_reserve(fhe_ctx *c, uint32_t max_batch) {
+  if (!c) return FHE_ERR_INVALID;
+  size_t need = (size_t)sizeof(u64) * c->n * max_batch * 2 * c->L;  // rotate / mul scratch
+  if (c->K) need += keyswitch_ws_bytes(c, max_batch);
+  if (c->nB) need = std::max(need, bfv_mul_ws_bytes(c, max_batch));
+  void *p;
+  return ctx_workspace(c, need, &p);
+}
+
+int fhe_dev_alloc(fhe_ctx *c, size_t bytes, void **out) {
+  if (!c || !out) return FHE_ERR_INVALID;
+  return fhe_check(c, hipMalloc(out, bytes), "hipMalloc");
+}
+int fhe_dev_free(fhe_ctx *c, void *ptr) {
+  if (!c) return FHE_ERR_INVALID;
+  return fhe_check(c, hipFree(ptr), "hipFree");
+}
+int fhe_memcpy_h2d(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return FHE_ERR_INVALID;
+  return fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream), "h2d");
+}
+int fhe_memcpy_d2h(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return FHE_ERR_INVALID;
+  int rc = fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream), "d2h");
+  if (rc) return rc;
+  return fhe_check(c, hipStreamSynchronize(c->stream), "d2h sync");
+}
+
+static int check_range(fhe_ctx *c, const void *p, uint32_t mod_begin, uint32_t n_limbs) {
+  if (!c) return FHE_ERR_INVALID;
+  if (!p) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
+  if (n_limbs == 0 || mod_begin + n_limbs > c->nmod) return fhe_fail(c, FHE_ERR_INVALID, "modulus range");
+  return FHE_OK;
+}
+
+int fhe_ntt_fwd(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs) {
+  int rc = check_range(c, data, mod_begin, n_limbs);
+  if (rc) return rc;
+  return ntt_launch(c, LimbMap{data, n_limbs, n_limbs, 0, n_limbs, 0, mod_begin, n_polys}, false);
+}
+int fhe_ntt_inv(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs) {
+  int rc = check_range(c, data, mod_begin, n_limbs);
+  if (rc) return rc;
+  return ntt_launch(c, LimbMap{data, n_limbs, n_limbs, 0, n_limbs, 0, mod_begin, n_polys}, true);
+}
+
+static int ew(fhe_ctx *c, EwOp op, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_polys,
+              uint32_t mod_begin, uint32_t n_limbs) {
+  int rc = check_range(c, a, mod_begin, n_limbs);
+  if (rc) return rc;
+  if (!b || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
+  return ew_launch(c, op, a, b, out, n_polys, mod_begin, n_limbs);
+}
+int fhe_poly_add(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n, uint32_t mb, uint32_t nl) {
+  return ew(c, EwOp::Add, a, b, out, n, mb, nl);
+}
+int fhe_poly_sub(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n, uint32_t mb, uint32_t nl) {
+  return ew(c, EwOp::Sub, a, b, out, n, mb, nl);
+}
+int fhe_poly_mul(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n, uint32_t mb, uint32_t nl) {
+  return ew(c, EwOp::Mul, a, b, out, n, mb, nl);
+}
+
+int fhe_base_conv(fhe_ctx *c, const uint64_t *src, const uint32_t *src_mods, uint32_t n_src, uint64_t *dst,
+                  const uint32_t *dst_mods, uint32_t n_dst, uint32_t n) {
+  if (!c || !src || !dst || !src_mods || !dst_mods) return fhe_fail(c, FHE_ERR_INVALID, "null argument");
+  if (n_src == 0 || n_src > 16 || n_dst == 0) return fhe_fail(c, FHE_ERR_INVALID, "conversion sizes");
+  std::vector<u32> s(src_mods, src_mods + n_src), d(dst_mods, dst_mods + n_dst);
+  for (u32 x : s)
+    if (x >= c->nmod) return fhe_fail(c, FHE_ERR_INVALID, "modulus id");
+  for (u32 x : d)
+    if (x >= c->nmod) return fhe_fail(c, FHE_ERR_INVALID, "modulus id");
+  static thread_local std::map<std::pair<const fhe_ctx *, std::vector<u32>>, ConvTab> cache;
+  std::vector<u32> key(s);
+  key.push_back(~0u);
+  key.insert(key.end(), d.begin(), d.end());
+  auto it = cache.find({c, key});
+  ConvTab t;
+  if (it == cache.end()) {
+    t = make_conv_tab(c, s, d);
+    if (!t.h) return fhe_fail(c, FHE_ERR_OOM, "conv table");
+    cache[{c, key}] = t;
+  } else {
+    t = it->second;
+  }
+  return conv_launch(c, t, src, n_src, dst, n_dst, n);
+}
+
+int fhe_fill_uniform(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs,
+                     uint64_t seed) {
+  int rc = check_range(c, data, mod_begin, n_limbs);
+  if (rc) return rc;
+  return fill_uniform_launch(c, data, n_polys, mod_begin, n_limbs, seed);
+}
+
+int fhe_add(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct) {
+  return ew(c, EwOp::Add, a, b, out, 2 * n_ct, 0, c ? c->L : 1);
+}
+int fhe_sub(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct) {
+  return ew(c, EwOp::Sub, a, b, out, 2 * n_ct, 0, c ? c->L : 1);
+}
+
+static int need_ks(fhe_ctx *c, const void *a, const void *k, const void *out) {
+  if (!c) return FHE_ERR_INVALID;
+  if (!a || !k || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
+  if (c->K == 0) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "context has no special primes (K = 0)");
+  return FHE_OK;
+}
+
+int fhe_mul_relin(fhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk, uint64_t *out,
+                  uint32_t n_ct) {
+  int rc = need_ks(c, a, rlk, out);
+  if (rc) return rc;
+  if (!b) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
+  if (!n_ct) return FHE_OK;
+  if (c->params.scheme == FHE_SCHEME_BFV) return bfv_mul_relin_impl(c, a, b, rlk, out, n_ct);
+  const size_t LN = (size_t)c->L * c->n;
+  void *ws;
+  if ((rc = ctx_workspace(c, sizeof(u64) * n_ct * LN + keyswitch_ws_bytes(c, n_ct), &ws))) return rc;
+  u64 *d2 = (u64 *)ws;
+  if ((rc = tensor_launch(c, a, 2 * LN, LN, b, 2 * LN, LN, out, 2 * LN, LN, d2, LN, n_ct, c->L, 0))) return rc;
+  return keyswitch_ex(c, d2, c->L, rlk, out, out, n_ct, 3u, true, d2 + n_ct * LN);
+}
+
+int fhe_keyswitch(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n) {
+  int rc = need_ks(c, d, ksk, out);
+  if (rc) return rc;
+  if (!n) return FHE_OK;
+  void *ws;
+  if ((rc = ctx_workspace(c, keyswitch_ws_bytes(c, n), &ws))) return rc;
+  return keyswitch_ex(c, d, c->L, ksk, out, out, n, 0u, c->params.scheme == FHE_SCHEME_CKKS, (u64 *)ws);
+}
+
+int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out, uint32_t n_ct) {
+  int rc = need_ks(c, ct, gk, out);
+  if (rc) return rc;
+  if ((g & 1) == 0 || g >= 2 * c->n) return fhe_fail(c, FHE_ERR_INVALID, "galois element must be odd and < 2N");
+  if (!n_ct) return FHE_OK;
+  const size_t LN = (size_t)c->L * c->n;
+  void *ws;
+  if ((rc = ctx_workspace(c, sizeof(u64) * n_ct * 2 * LN + keyswitch_ws_bytes(c, n_ct), &ws))) return rc;
+  u64 *tmp = (u64 *)ws;
+  const bool ntt = c->params.scheme == FHE_SCHEME_CKKS;
+  if ((rc = automorph_launch(c, ct, tmp, g, 2 * n_ct, ntt))) return rc;
+  return keyswitch_ex(c, tmp + LN, 2 * c->L, gk, tmp, out, n_ct, 1u, ntt, tmp + n_ct * 2 * LN);
+}
+
+int fhe_galois_elt(const fhe_ctx *c, int32_t steps, uint32_t *out) {
+  if (!c || !out) return FHE_ERR_INVALID;
+  const int64_t ord = c->n / 2;
+  int64_t s = steps % ord;
+  if (s < 0) s += ord;
+  *out = (u32)hpow(5, (u64)s, 2ull * c->n);
+  return FHE_OK;
+}
+
+int fhe_bcast_key(fhe_ctx *c, uint64_t *key, size_t words, void *comm, int root) {
+  if (!c || !key || !comm) return fhe_fail(c, FHE_ERR_INVALID, "null argument");
+  ncclResult_t r = ncclBroadcast(key, key, words, ncclUint64, root, (ncclComm_t)comm, c->stream);
+  if (r != ncclSuccess) return fhe_fail(c, FHE_ERR_DEVICE, std::string("ncclBroadcast: ") + ncclGetErrorString(r));
+  return FHE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,127 @@
+/*
+ * fhe_backend.h -- C ABI of the MI355X-native FHE ciphertext-op backend.
+ *
+ * This is the build's `include/plugins` operator surface (BASELINE.json
+ * north_star).  herdsman (/root/reference) has no FHE operator surface of its
+ * own: its only plugin is the gRPC token processor
+ * (/root/reference/include/plugins/token_auth_metadata_processor.hpp:9-31),
+ * and the arithmetic runs in remote workers reached through
+ * IWorkerGroup::schedule_task (/root/reference/include/execution/worker/
+ * i_worker_group.hpp:46; GrpcWorkerGroup::schedule_task at
+ * /root/reference/src/execution/worker/grpc/grpc_worker_group.cpp:70-105).
+ * Each entry point below REPLACES the remote `Worker.map` evaluation of one
+ * ciphertext operation (grpc_worker_group.cpp:85 `stub->Asyncmap`) with an
+ * in-process HIP call; the host-side caller is the GPU worker group
+ * (herdsman_amd/host/gpu_worker_group.hpp), which keeps the IWorkerGroup
+ * contract, so src/execution's Executor and the proto/service layer are
+ * unchanged.
+ *
+ * Conventions (also those of the CPU oracle, oracle/fhe_oracle.h):
+ *  - all words are u64; a polynomial is limb-major [limb][N]; batches are
+ *    [item][poly][limb][N]; every pointer is DEVICE memory unless noted;
+ *  - modulus index space: [0,L) = Q (ciphertext primes), [L,L+K) = P
+ *    (special primes), then for BFV the BEHZ base Bsk (L+1 primes);
+ *  - forward NTT: natural in, bit-reversed out, out[k] = a(psi^(2brv(k)+1)),
+ *    psi = smallest primitive 2N-th root; outputs canonical in [0,q);
+ *  - CKKS ciphertexts are kept in NTT form, BFV ciphertexts in coefficient
+ *    form; (c0, c1) decrypts as c0 + c1*s;
+ *  - switching keys: [dnum][2][L+K][N] NTT form (see oracle/fhe_oracle.h).
+ *  - every function returns FHE_OK (0) or a negative FHE_ERR_*; the message
+ *    is available from fhe_last_error(ctx).  No C++ exception crosses the ABI
+ *    (matching IWorkerGroup's "no exceptions cross the seam",
+ *    /root/reference/src/execution/executor/executor.cpp:168-178).
+ *  - calls on one context are serialised by the caller; work is enqueued on
+ *    the context's stream (fhe_set_stream) and is asynchronous.
+ */
+#ifndef HERDSMAN_PLUGINS_FHE_BACKEND_H
+#define HERDSMAN_PLUGINS_FHE_BACKEND_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FHE_OK 0
+#define FHE_ERR_INVALID -1
+#define FHE_ERR_DEVICE -2
+#define FHE_ERR_OOM -3
+#define FHE_ERR_UNSUPPORTED -4
+
+#define FHE_SCHEME_CKKS 0u
+#define FHE_SCHEME_BFV 1u
+
+typedef struct fhe_ctx fhe_ctx;
+
+typedef struct fhe_params {
+  uint32_t scheme;         /* FHE_SCHEME_CKKS or FHE_SCHEME_BFV */
+  uint32_t log_n;          /* ring degree N = 2^log_n, 10..17 */
+  uint32_t num_q;          /* L: ciphertext primes */
+  uint32_t num_p;          /* K: special primes for hybrid key switching */
+  uint32_t dnum;           /* number of key-switching digits, alpha = ceil(L/dnum) */
+  uint32_t q_bits;         /* bit size for generated Q primes (<= 61) */
+  uint32_t p_bits;         /* bit size for generated P / Bsk primes (<= 61) */
+  uint32_t reserved;
+  uint64_t plain_modulus;  /* t (BFV only) */
+  const uint64_t *moduli;  /* HOST pointer, optional explicit moduli in index-space order; NULL = generate */
+} fhe_params;
+
+/* ---- context -------------------------------------------------------- */
+int fhe_ctx_create(const fhe_params *params, int device, fhe_ctx **out);
+void fhe_ctx_destroy(fhe_ctx *ctx);
+const char *fhe_last_error(const fhe_ctx *ctx);
+/* number of moduli in the index space, and the moduli themselves (HOST out) */
+int fhe_ctx_moduli(const fhe_ctx *ctx, uint64_t *out, uint32_t cap, uint32_t *count);
+int fhe_set_stream(fhe_ctx *ctx, void *hip_stream);
+int fhe_synchronize(fhe_ctx *ctx);
+/* pre-size the context's scratch so later ops never allocate (graph capture) */
+int fhe_reserve(fhe_ctx *ctx, uint32_t max_batch);
+
+/* ---- device memory helpers (for callers without their own allocator) -- */
+int fhe_dev_alloc(fhe_ctx *ctx, size_t bytes, void **out);
+int fhe_dev_free(fhe_ctx *ctx, void *ptr);
+int fhe_memcpy_h2d(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
+int fhe_memcpy_d2h(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
+
+/* ---- RNS primitives: data [n_polys][n_limbs][N]; limb l uses modulus mod_begin+l */
+int fhe_ntt_fwd(fhe_ctx *ctx, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs);
+int fhe_ntt_inv(fhe_ctx *ctx, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs);
+int fhe_poly_add(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_polys,
+                 uint32_t mod_begin, uint32_t n_limbs);
+int fhe_poly_sub(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_polys,
+                 uint32_t mod_begin, uint32_t n_limbs);
+int fhe_poly_mul(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_polys,
+                 uint32_t mod_begin, uint32_t n_limbs);
+/* fast base conversion: src [n][n_src][N] over moduli src_mods -> dst [n][n_dst][N] (index lists on HOST) */
+int fhe_base_conv(fhe_ctx *ctx, const uint64_t *src, const uint32_t *src_mods, uint32_t n_src, uint64_t *dst,
+                  const uint32_t *dst_mods, uint32_t n_dst, uint32_t n);
+/* deterministic uniform fill: word w of the buffer = hi64(splitmix64(seed+(w+1)*phi) * q) */
+int fhe_fill_uniform(fhe_ctx *ctx, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs,
+                     uint64_t seed);
+
+/* ---- ciphertext operations (the operator surface) ---------------------
+ * ct buffers: [n_ct][2][L][N]; keys: [dnum][2][L+K][N] */
+int fhe_add(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct);
+int fhe_sub(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct);
+/* ct x ct multiply + relinearize (CKKS: NTT-domain tensor; BFV: BEHZ) */
+int fhe_mul_relin(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, const uint64_t *rlk, uint64_t *out,
+                  uint32_t n_ct);
+/* hybrid key switch: d [n][L][N] -> out [n][2][L][N] (same domain as the scheme's ciphertexts) */
+int fhe_keyswitch(fhe_ctx *ctx, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n);
+/* automorphism X -> X^galois_elt followed by key switching with the Galois key */
+int fhe_rotate(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const uint64_t *gk, uint64_t *out,
+               uint32_t n_ct);
+/* 5^steps mod 2N (steps may be negative); conjugation is 2N-1 */
+int fhe_galois_elt(const fhe_ctx *ctx, int32_t steps, uint32_t *out);
+
+/* ---- multi-GPU ---------------------------------------------------------
+ * Broadcast an evaluation key (words u64 in device memory) from `root` to all
+ * ranks of an RCCL communicator (ncclComm_t passed as void*).  The only
+ * collective the backend uses. */
+int fhe_bcast_key(fhe_ctx *ctx, uint64_t *key, size_t words, void *nccl_comm, int root);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

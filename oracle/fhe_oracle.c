@@ -630,33 +630,42 @@ static void bfv_mul_relin_one(const orc_ctx *c, const behz_tab *B, const uint64_
   free(xq); free(xb); free(eq); free(eb); free(r); free(ks);
 }
 
+static void ckks_mul_relin_one(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
+                               uint64_t *out) {
+  const size_t L = c->L, N = c->n;
+  uint64_t *d = malloc(sizeof(uint64_t) * 3 * L * N);
+  uint64_t *ks = malloc(sizeof(uint64_t) * 2 * L * N);
+  const uint64_t *a0 = a, *a1 = a0 + L * N, *b0 = b, *b1 = b0 + L * N;
+  for (uint32_t l = 0; l < L; ++l) {
+    const uint64_t q = c->m[l].q;
+    for (uint32_t k = 0; k < N; ++k) {
+      size_t o = (size_t)l * N + k;
+      d[o] = mulmod(a0[o], b0[o], q);
+      d[L * N + o] = addmod(mulmod(a0[o], b1[o], q), mulmod(a1[o], b0[o], q), q);
+      d[2 * L * N + o] = mulmod(a1[o], b1[o], q);
+    }
+  }
+  keyswitch_one(c, d + 2 * L * N, rlk, ks, 1);
+  orc_add(c, d, ks, out, 2, 0, (uint32_t)L);
+  free(d); free(ks);
+}
+
+/* items are independent: one OpenMP thread per ciphertext (the inner
+ * per-limb loops then run serially, nested parallelism being off). */
 void orc_mul_relin(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
                    uint64_t *out, uint32_t n_ct) {
   const size_t L = c->L, N = c->n, CT = 2 * L * N;
+  behz_tab *B = NULL;
   if (c->scheme == ORC_SCHEME_BFV) {
-    behz_tab *B = malloc(sizeof(behz_tab));
+    B = malloc(sizeof(behz_tab));
     behz_init(c, B);
-    for (uint32_t i = 0; i < n_ct; ++i) bfv_mul_relin_one(c, B, a + i * CT, b + i * CT, rlk, out + i * CT);
-    free(B);
-    return;
   }
-  uint64_t *d = malloc(sizeof(uint64_t) * 3 * L * N);
-  uint64_t *ks = malloc(sizeof(uint64_t) * 2 * L * N);
-  for (uint32_t i = 0; i < n_ct; ++i) {
-    const uint64_t *a0 = a + i * CT, *a1 = a0 + L * N, *b0 = b + i * CT, *b1 = b0 + L * N;
-    for (uint32_t l = 0; l < L; ++l) {
-      const uint64_t q = c->m[l].q;
-      for (uint32_t k = 0; k < N; ++k) {
-        size_t o = (size_t)l * N + k;
-        d[o] = mulmod(a0[o], b0[o], q);
-        d[L * N + o] = addmod(mulmod(a0[o], b1[o], q), mulmod(a1[o], b0[o], q), q);
-        d[2 * L * N + o] = mulmod(a1[o], b1[o], q);
-      }
-    }
-    keyswitch_one(c, d + 2 * L * N, rlk, ks, 1);
-    orc_add(c, d, ks, out + i * CT, 2, 0, (uint32_t)L);
+#pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
+  for (long i = 0; i < (long)n_ct; ++i) {
+    if (B) bfv_mul_relin_one(c, B, a + i * CT, b + i * CT, rlk, out + i * CT);
+    else ckks_mul_relin_one(c, a + i * CT, b + i * CT, rlk, out + i * CT);
   }
-  free(d); free(ks);
+  free(B);
 }
 
 void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,

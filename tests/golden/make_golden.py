@@ -52,13 +52,13 @@ def gen_ntt(rng):
 
 
 def gen_conv(rng):
-    log_n = 8
+    log_n = 10
     n = 1 << log_n
     mods = M.gen_primes(60, log_n, 4) + M.gen_primes(61, log_n, 3)
     src, dst = [0, 1, 2, 3], [4, 5, 6]
     x = rand_limbs(rng, [mods[i] for i in src], n)
     y = M.base_conv(x, [mods[i] for i in src], [mods[i] for i in dst])
-    np.savez(os.path.join(HERE, "conv_n256.npz"), log_n=np.uint32(log_n), moduli=arr(mods),
+    np.savez(os.path.join(HERE, "conv_n1024.npz"), log_n=np.uint32(log_n), moduli=arr(mods),
              src=np.array(src, dtype=np.uint32), dst=np.array(dst, dtype=np.uint32), x=arr(x), y=arr(y))
 
 

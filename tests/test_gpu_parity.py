@@ -1,0 +1,272 @@
+"""HIP backend (libherdsman_fhe.so, through the C ABI) vs the CPU oracle.
+
+Bit-exact for every op (all arithmetic is integer mod q).  Three kinds of
+evidence:
+  * golden fixtures (tests/golden/, big-int model) at N = 1024;
+  * the oracle on identical seeded inputs at the BASELINE.json configs
+    C2 (NTT, N=2^14 L=4), C3 (BFV mul+relin, N=2^15 L=8), C4 (CKKS rotate,
+    N=2^16 L=12 dnum=3) and the metric config (CKKS mul+relin N=2^16 L=12);
+  * scheme-level decryption identities with real keys.
+"""
+import math
+import os
+import random
+
+import numpy as np
+import pytest
+
+from fhe_math import automorph_int, crt_centered, negacyclic_int, to_rns
+from oracle_ffi import Oracle, SCHEME_BFV, SCHEME_CKKS
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def hb():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    import herdsman_amd.backend as hb
+
+    hb.load_library()
+    return hb
+
+
+def pair(hb, scheme, log_n, L, K=0, dnum=1, t=0, moduli=None):
+    o = Oracle(scheme, log_n, L, K, dnum, t=t, moduli=moduli)
+    g = hb.Context(scheme, log_n, L, K, dnum, t=t, moduli=o.moduli)
+    assert np.array_equal(g.moduli, o.moduli)
+    return o, g
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+# --------------------------------------------------------------------- NTT
+def test_ntt_golden(hb):
+    g = load("ntt_n1024.npz")
+    o, c = pair(hb, SCHEME_CKKS, 10, 3, moduli=g["moduli"])
+    x = hb.to_device(g["x"])
+    c.ntt_fwd(x)
+    assert np.array_equal(hb.to_host(x), g["y"])
+    c.ntt_inv(x)
+    assert np.array_equal(hb.to_host(x), g["x"])
+
+
+@pytest.mark.parametrize("log_n,L,polys", [(10, 2, 3), (11, 2, 1), (12, 3, 2), (13, 2, 1), (14, 4, 2),
+                                            (15, 3, 1), (16, 4, 2), (17, 2, 1)])
+def test_ntt_vs_oracle(hb, log_n, L, polys):
+    o, c = pair(hb, SCHEME_CKKS, log_n, L)
+    x = o.uniform((polys, L, 1 << log_n), seed=log_n * 131 + L)
+    want = o.ntt_fwd(x)
+    d = hb.to_device(x)
+    c.ntt_fwd(d)
+    assert np.array_equal(hb.to_host(d), want)
+    c.ntt_inv(d)
+    assert np.array_equal(hb.to_host(d), x)
+    # inverse from an arbitrary (non-NTT-image) canonical input too
+    d = hb.to_device(x)
+    c.ntt_inv(d)
+    assert np.array_equal(hb.to_host(d), o.ntt_inv(x))
+
+
+def test_ntt_c2_config(hb):
+    """BASELINE.json configs[1]: forward+inverse NTT, N=2^14, 4 limbs, bit-exact vs CPU."""
+    o, c = pair(hb, SCHEME_CKKS, 14, 4)
+    x = o.uniform((8, 4, 1 << 14), seed=2)
+    d = hb.to_device(x)
+    c.ntt_fwd(d)
+    assert np.array_equal(hb.to_host(d), o.ntt_fwd(x))
+    c.ntt_inv(d)
+    assert np.array_equal(hb.to_host(d), x)
+
+
+def test_ntt_p_part_mod_offset(hb):
+    o, c = pair(hb, SCHEME_CKKS, 12, 3, K=2, dnum=3)
+    x = o.uniform((2, 2, 1 << 12), seed=9, mod_begin=3)
+    d = hb.to_device(x)
+    c.ntt_fwd(d, mod_begin=3)
+    assert np.array_equal(hb.to_host(d), o.ntt_fwd(x, mod_begin=3))
+
+
+def test_fill_uniform_matches_oracle(hb):
+    o, c = pair(hb, SCHEME_CKKS, 12, 3)
+    d = hb.empty((2, 3, 1 << 12))
+    c.fill_uniform(d, seed=77)
+    assert np.array_equal(hb.to_host(d), o.uniform((2, 3, 1 << 12), seed=77))
+
+
+def test_poly_ops(hb):
+    o, c = pair(hb, SCHEME_CKKS, 11, 3)
+    a = o.uniform((2, 3, 1 << 11), seed=1)
+    b = o.uniform((2, 3, 1 << 11), seed=2)
+    da, db, dout = hb.to_device(a), hb.to_device(b), hb.empty(a.shape)
+    for op in ("add", "sub", "mul"):
+        c.poly_op(op, da, db, dout)
+        want = np.zeros_like(a)
+        getattr(o.lib, f"orc_{op}")(o.h, a, b, want, 2, 0, 3)
+        assert np.array_equal(hb.to_host(dout), want), op
+
+
+def test_base_conv_golden(hb):
+    g = load("conv_n1024.npz")
+    c = hb.Context(SCHEME_CKKS, int(g["log_n"]), len(g["moduli"]), moduli=g["moduli"])
+    x = hb.to_device(g["x"][None])
+    y = hb.empty((1, len(g["dst"]), 1 << int(g["log_n"])))
+    c.base_conv(x, g["src"], y, g["dst"])
+    assert np.array_equal(hb.to_host(y)[0], g["y"])
+
+
+# -------------------------------------------------------------------- CKKS
+def test_ckks_golden(hb):
+    g = load("ckks_n1024_l4.npz")
+    o, c = pair(hb, SCHEME_CKKS, 10, 4, 2, 2, moduli=g["moduli"])
+    a, b = hb.to_device(g["a"][None]), hb.to_device(g["b"][None])
+    rlk, gk = hb.to_device(g["rlk"]), hb.to_device(g["gk"])
+    out = hb.empty(a.shape)
+    c.mul_relin(a, b, rlk, out)
+    assert np.array_equal(hb.to_host(out)[0], g["out_mul"])
+    c.rotate(a, int(g["g"]), gk, out)
+    assert np.array_equal(hb.to_host(out)[0], g["out_rot"])
+    c.rotate(b, int(g["g_conj"]), gk, out)
+    assert np.array_equal(hb.to_host(out)[0], g["out_conj"])
+
+
+@pytest.mark.parametrize("log_n,L,K,dnum,n_ct", [(12, 5, 2, 3, 3), (16, 12, 4, 3, 2)])
+def test_ckks_mul_relin_vs_oracle(hb, log_n, L, K, dnum, n_ct):
+    """(16, 12, 4, 3) is the BASELINE metric config (ct-mult+relin, N=2^16, L=12)."""
+    o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum)
+    a = o.uniform((n_ct, 2, L, 1 << log_n), seed=10)
+    b = o.uniform((n_ct, 2, L, 1 << log_n), seed=11)
+    rlk = o.uniform(o.key_shape(), seed=12)
+    want = o.mul_relin(a, b, rlk)
+    da, db, dk, dout = hb.to_device(a), hb.to_device(b), hb.to_device(rlk), hb.empty(a.shape)
+    c.mul_relin(da, db, dk, dout)
+    assert np.array_equal(hb.to_host(dout), want)
+    # in-place output aliasing the first operand
+    c.mul_relin(da, db, dk, da)
+    assert np.array_equal(hb.to_host(da), want)
+
+
+def test_ckks_rotate_c4(hb):
+    """BASELINE.json configs[3]: CKKS rotate + hybrid KS (dnum=3), N=2^16, L=12."""
+    o, c = pair(hb, SCHEME_CKKS, 16, 12, 4, 3)
+    ct = o.uniform((2, 2, 12, 1 << 16), seed=20)
+    gk = o.uniform(o.key_shape(), seed=21)
+    for steps in (1, -7):
+        g = o.galois_elt(steps)
+        want = o.rotate(ct, g, gk)
+        dct, dgk, dout = hb.to_device(ct), hb.to_device(gk), hb.empty(ct.shape)
+        c.rotate(dct, g, dgk, dout)
+        assert np.array_equal(hb.to_host(dout), want), steps
+
+
+def test_keyswitch_vs_oracle(hb):
+    o, c = pair(hb, SCHEME_CKKS, 13, 7, 3, 3)  # ragged digits: alpha=3, last digit has 1 limb
+    d = o.uniform((2, 7, 1 << 13), seed=30)
+    k = o.uniform(o.key_shape(), seed=31)
+    want = o.keyswitch(d, k)
+    dout = hb.empty(want.shape)
+    c.keyswitch(hb.to_device(d), hb.to_device(k), dout)
+    assert np.array_equal(hb.to_host(dout), want)
+
+
+def test_ckks_real_keys_decrypt(hb):
+    o, c = pair(hb, SCHEME_CKKS, 12, 4, 2, 2)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    s = o.secret(3)
+    s_qp = o.signed_to_rns(s, 0, o.L + o.K, ntt=True)
+    sq = np.array([[(int(x) * int(x)) % int(o.moduli[i]) for x in s_qp[i]] for i in range(o.L + o.K)],
+                  dtype=np.uint64)
+    rlk = o.switch_key(sq, s_qp, seed=4)
+    rng = random.Random(5)
+    delta = 1 << 30
+    u1 = [rng.randint(-4, 4) for _ in range(o.n)]
+    u2 = [rng.randint(-4, 4) for _ in range(o.n)]
+    c1 = o.encrypt(to_rns([delta * x for x in u1], Q), s_qp, 1)
+    c2 = o.encrypt(to_rns([delta * x for x in u2], Q), s_qp, 2)
+    dout = hb.empty((1, 2, o.L, o.n))
+    c.mul_relin(hb.to_device(c1[None]), hb.to_device(c2[None]), hb.to_device(rlk), dout)
+    dec = crt_centered(o.decrypt(hb.to_host(dout)[0], s_qp), Q)
+    want = [delta * delta * v for v in negacyclic_int(u1, u2)]
+    assert max(abs(x - y) for x, y in zip(dec, want)) < 2 ** 56
+
+
+# --------------------------------------------------------------------- BFV
+def test_bfv_golden(hb):
+    g = load("bfv_n1024_l4.npz")
+    o, c = pair(hb, SCHEME_BFV, 10, 4, 2, 2, t=int(g["t"]), moduli=g["moduli"])
+    a, b = hb.to_device(g["a"][None]), hb.to_device(g["b"][None])
+    rlk = hb.to_device(g["rlk"])
+    out = hb.empty(a.shape)
+    c.add(a, b, out)
+    assert np.array_equal(hb.to_host(out)[0], g["out_add"])
+    c.mul_relin(a, b, rlk, out)
+    assert np.array_equal(hb.to_host(out)[0], g["out_mul"])
+    c.rotate(a, int(g["g"]), rlk, out)
+    assert np.array_equal(hb.to_host(out)[0], g["out_rot"])
+
+
+def test_bfv_c1_add(hb):
+    """BASELINE.json configs[0]: BFV add, N=4096, one 60-bit prime."""
+    o, c = pair(hb, SCHEME_BFV, 12, 1, 1, 1, t=65537)
+    a = o.uniform((4, 2, 1, 4096), seed=40)
+    b = o.uniform((4, 2, 1, 4096), seed=41)
+    out = hb.empty(a.shape)
+    c.add(hb.to_device(a), hb.to_device(b), out)
+    assert np.array_equal(hb.to_host(out), o.ct_add(a, b))
+
+
+def test_bfv_mul_relin_c3(hb):
+    """BASELINE.json configs[2]: BFV ct x ct multiply + relinearize, N=2^15, L=8."""
+    o, c = pair(hb, SCHEME_BFV, 15, 8, 4, 2, t=65537)
+    a = o.uniform((2, 2, 8, 1 << 15), seed=50)
+    b = o.uniform((2, 2, 8, 1 << 15), seed=51)
+    rlk = o.uniform(o.key_shape(), seed=52)
+    want = o.mul_relin(a, b, rlk)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(rlk), dout)
+    assert np.array_equal(hb.to_host(dout), want)
+
+
+def test_bfv_real_keys_exact(hb):
+    t = 65537
+    o, c = pair(hb, SCHEME_BFV, 12, 3, 3, 1, t=t)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    Qp = math.prod(Q)
+    s = o.secret(8)
+    s_qp = o.signed_to_rns(s, 0, o.L + o.K, ntt=True)
+    sq = np.array([[(int(x) * int(x)) % int(o.moduli[i]) for x in s_qp[i]] for i in range(o.L + o.K)],
+                  dtype=np.uint64)
+    rlk = o.switch_key(sq, s_qp, seed=9)
+    rng = random.Random(10)
+    m1 = [rng.randrange(t) for _ in range(o.n)]
+    m2 = [rng.randrange(t) for _ in range(o.n)]
+    delta = Qp // t
+    c1 = o.encrypt(to_rns([delta * x for x in m1], Q), s_qp, 11)
+    c2 = o.encrypt(to_rns([delta * x for x in m2], Q), s_qp, 12)
+    dout = hb.empty((1, 2, o.L, o.n))
+    c.mul_relin(hb.to_device(c1[None]), hb.to_device(c2[None]), hb.to_device(rlk), dout)
+    v = crt_centered(o.decrypt(hb.to_host(dout)[0], s_qp), Q)
+    dec = [((t * x + Qp // 2) // Qp) % t for x in v]
+    assert dec == [x % t for x in negacyclic_int(m1, m2)]
+    g = o.galois_elt(3)
+    gk = o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=13)
+    c.rotate(hb.to_device(c1[None]), g, hb.to_device(gk), dout)
+    v = crt_centered(o.decrypt(hb.to_host(dout)[0], s_qp), Q)
+    assert [((t * x + Qp // 2) // Qp) % t for x in v] == [x % t for x in automorph_int(m1, g)]
+
+
+# ---------------------------------------------------------------- errors
+def test_errors_are_loud(hb):
+    c = hb.Context(SCHEME_CKKS, 12, 2)
+    x = hb.empty((1, 2, 1 << 12))
+    with pytest.raises(hb.FheBackendError):
+        c.ntt_fwd(x, mod_begin=5)  # out of modulus range
+    with pytest.raises(hb.FheBackendError):
+        c.mul_relin(hb.empty((1, 2, 2, 1 << 12)), hb.empty((1, 2, 2, 1 << 12)), x, hb.empty((1, 2, 2, 1 << 12)))
+    with pytest.raises(hb.FheBackendError):
+        hb.Context(SCHEME_CKKS, 9, 2)  # N below the supported range

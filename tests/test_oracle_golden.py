@@ -35,7 +35,7 @@ def test_ntt_golden():
 
 
 def test_base_conv_golden():
-    g = load("conv_n256.npz")
+    g = load("conv_n1024.npz")
     o = Oracle(SCHEME_CKKS, int(g["log_n"]), len(g["moduli"]), moduli=g["moduli"])
     y = o.base_conv(g["x"], g["src"], g["dst"])
     assert np.array_equal(y[0], g["y"])
