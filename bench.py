@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Headline benchmark: CKKS ct-mult+relin/s at N=2^16, L=12 (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+
+One step = one fhe_mul_relin call over B independent ciphertext pairs per GPU
+(N=2^16, L=12 primes of 60 bits, K=4 special primes of 61 bits, dnum=3 hybrid
+key switching), inputs already resident in HBM (generated on device with the
+backend's SplitMix64 fill).  Multi-GPU: one process per GPU (torchrun), the
+relinearisation key is generated on rank 0 and broadcast once over RCCL
+(the only collective), then every rank works on its own shard with no
+communication ("scaling": "weak").  value = ct-mults of all ranks / max-rank time.
+
+Extra fields:
+  roofline     -- the dominant kernel group, the forward NTT (column + row pass
+                  kernels, one fhe_ntt_fwd launch over the batch's limbs),
+                  timed with HIP events on the backend's stream; algorithmic
+                  bytes = 2 * N * 8 per limb-NTT (read + write the residue once).
+  cpu_baseline -- the CPU oracle (oracle/fhe_oracle.c, OpenMP over ciphertexts)
+                  on a bounded sample of the same workload, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "ct-mult+relin/sec at N=2^16 L=12; achieved HBM GB/s vs 8 TB/s peak"
+LOG_N, L, K, DNUM = 16, 12, 4, 3
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="ct-mults per GPU per step")
+    ap.add_argument("--ntt-reps", type=int, default=20)
+    ap.add_argument("--cpu-sample", type=int, default=4096, help="max ct-mults in the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline duration")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "ntt_traffic.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import herdsman_amd.backend as hb
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    ctx = hb.Context(hb.SCHEME_CKKS, LOG_N, L, K, DNUM, device=local)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream)
+    n = 1 << LOG_N
+    B = args.batch
+    ctx.reserve(B)
+
+    # relinearisation key: rank 0 makes it, RCCL broadcast to everyone else
+    rlk = hb.empty(ctx.key_shape(), device=dev)
+    if rank == 0:
+        ctx.fill_uniform(rlk, seed=0x524C4B)
+    torch.cuda.synchronize(dev)
+    t_b = time.perf_counter()
+    if world > 1:
+        dist.broadcast(rlk, src=0)
+    torch.cuda.synchronize(dev)
+    key_bcast_ms = (time.perf_counter() - t_b) * 1e3
+
+    a = hb.empty((B, 2, L, n), device=dev)
+    b = hb.empty((B, 2, L, n), device=dev)
+    out = hb.empty((B, 2, L, n), device=dev)
+    ctx.fill_uniform(a, seed=0x48455244 ^ (rank << 32) ^ 1)
+    ctx.fill_uniform(b, seed=0x48455244 ^ (rank << 32) ^ 2)
+
+    def step():
+        ctx.mul_relin(a, b, rlk, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total = world * B * args.steps
+    value = total / elapsed
+
+    # ---- dominant kernel group: forward NTT over the ModUp-sized batch (36 limbs per ct)
+    limbs = B * 3 * L  # the converted limbs of one batch's ModUp
+    x = hb.empty((limbs, 1, n), device=dev)
+    ctx.fill_uniform(x.view(B * 3, L, n), seed=99)
+    for _ in range(3):
+        ctx.ntt_fwd(x.view(B * 3, L, n))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.ntt_reps):
+        ctx.ntt_fwd(x.view(B * 3, L, n))
+    e1.record(stream)
+    e1.synchronize()
+    ntt_ms = e0.elapsed_time(e1) / args.ntt_reps
+    algo_bytes = limbs * 2 * n * 8
+    achieved = algo_bytes / (ntt_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            traffic = tj.get("hbm_bytes_per_limb_ntt")
+            if traffic is not None:
+                traffic = traffic * limbs
+        except Exception:
+            traffic = None
+    ntt_limb_per_s = limbs / (ntt_ms * 1e-3)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, ctx)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "ct-mult/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: uniform residues mod q (on-device SplitMix64), uniform relin key",
+            "config": {
+                "workload": "ckks_mul_relin",
+                "log_n": LOG_N, "L": L, "K": K, "dnum": DNUM,
+                "q_bits": 60, "p_bits": 61,
+                "batch_per_gpu": B, "global_batch": B * world,
+                "parallelism": f"shard{world}",
+            },
+            "roofline": {
+                "kernel": "ntt_fwd (ntt_pass col + row), N=2^16",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes": algo_bytes,
+                "launch_ms": round(ntt_ms, 4),
+            },
+            "ntt_fwd_limb_per_s": round(ntt_limb_per_s, 1),
+            "key_bcast_ms": round(key_bcast_ms, 3),
+            "algorithmic_GBps_ct_mult": round(value / world * 6 * L * n * 8 / 1e9, 1),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, ctx):
+    """CPU oracle (test infrastructure) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_ffi import Oracle, SCHEME_CKKS
+
+    o = Oracle(SCHEME_CKKS, LOG_N, L, K, DNUM, moduli=ctx.moduli)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    o.lib.orc_set_threads(threads)
+    s = max(threads, 1)
+    a = o.uniform((s, 2, L, 1 << LOG_N), seed=1)
+    b = o.uniform((s, 2, L, 1 << LOG_N), seed=2)
+    k = o.uniform(o.key_shape(), seed=3)
+    done, t0 = 0, time.perf_counter()
+    while True:  # ~args.cpu_seconds of CPU work, at least two rounds
+        o.mul_relin(a, b, k)
+        done += s
+        dt = time.perf_counter() - t0
+        if (dt >= args.cpu_seconds and done >= 2 * s) or done >= args.cpu_sample:
+            break
+    return {
+        "value": round(done / dt, 3),
+        "unit": "ct-mult/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{done} CKKS ct-mult+relin at N=2^16 L=12 K=4 dnum=3 in {dt:.1f} s "
+                  f"(batches of {s}, OpenMP one ciphertext per thread)",
+    }
+
+
+if __name__ == "__main__":
+    main()

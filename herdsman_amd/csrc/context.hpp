@@ -30,18 +30,17 @@ __host__ __device__ __forceinline__ u32 limbmap_limb(const LimbMap &m, u32 act) 
   return m.first + (act < m.skip_lo ? act : act + m.skip_len);
 }
 
-// Fast base conversion table (device): src moduli -> dst moduli.
+// Fast base conversion table (device): src moduli -> dst moduli, Montgomery
+// pre-scaled:  v_i = mont_mul(x_i, hinv[i]) = [x_i (S/s_i)^-1]_{s_i} exactly,
+// y_m = mont_reduce(sum_i v_i h[i][m]) = (sum_i v_i (S/s_i)) * R^(e-1) mod d_m
+// where h = (S/s_i) * R^e (e = 1: plain result, e = 2: result times R).
 struct ConvTab {
   u32 ns, nd;
   const u32 *src_mod; // [ns] modulus ids of the sources
   const u32 *dst_mod; // [nd] modulus ids of the destinations
-  const Tw *hinv;     // [ns] {(S/s_i)^-1 mod s_i, Shoup}
-  const u64 *h;       // [ns][nd] (S/s_i) mod d_m
+  const u64 *hinv;    // [ns] (S/s_i)^-1 * R mod s_i
+  const u64 *h;       // [ns][nd] (S/s_i) * R^e mod d_m
 };
-// host-side construction (ops.cpp); uploads into context-owned device memory
-ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst);
-
-struct BehzTabDev;  // defined in rns.hip
 
 struct fhe_ctx {
   fhe_params params{};
@@ -50,16 +49,17 @@ struct fhe_ctx {
   std::string err;
   u32 log_n = 0, n = 0, L = 0, K = 0, dnum = 0, alpha = 0, nB = 0, nmod = 0;
   u64 t = 0;
+  bool special = false;        // every modulus = 1 mod 2^32 (fast Montgomery)
   std::vector<u64> moduli;
-  // device-resident tables
+  // device-resident tables (constants in Montgomery form, x * 2^64 mod q)
   ModInfo *d_mods = nullptr;   // [nmod]
-  Tw *d_tw_fwd = nullptr;      // [nmod][N]  psi^brv(i)
-  Tw *d_tw_inv = nullptr;      // [nmod][N]  psi^-brv(i)
-  Tw *d_ninv = nullptr;        // [nmod]     N^-1
-  Tw *d_pinv = nullptr;        // [L]        P^-1 mod q_i
-  // ModUp tables per digit, ModDown table (device blobs + host descriptors)
-  ConvTab *d_modup = nullptr;  // device array [dnum]
-  ConvTab moddown{};
+  u64 *d_tw_fwd = nullptr;     // [nmod][N]  psi^brv(i) R
+  u64 *d_tw_inv = nullptr;     // [nmod][N]  psi^-brv(i) R
+  u64 *d_ninv = nullptr;       // [nmod]     N^-1 R
+  u64 *d_pinv = nullptr;       // [L]        P^-1 R mod q_i
+  u64 *d_r2 = nullptr;         // [nmod]     R^2 mod q (x -> x R)
+  ConvTab *d_modup = nullptr;  // device array [ceil(L/alpha)], h scaled by R^2
+  ConvTab moddown{};           // P -> Q, h scaled by R
   std::vector<void *> blobs;   // device allocations owned by the context
   void *behz = nullptr;        // BEHZ device constants (BFV)
   // scratch
@@ -67,11 +67,16 @@ struct fhe_ctx {
   size_t ws_bytes = 0;
 };
 
-// helpers shared by the translation units
+// helpers shared by the translation units (fhe_backend.cpp)
 int fhe_fail(fhe_ctx *c, int code, const std::string &msg);
 int fhe_check(fhe_ctx *c, hipError_t e, const char *what);
 void *ctx_upload(fhe_ctx *c, const void *host, size_t bytes);  // owned blob
 int ctx_workspace(fhe_ctx *c, size_t bytes, void **out);
+ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst, int r_exp);
+// host modular helpers
+u64 host_mulmod(u64 a, u64 b, u64 q);
+u64 host_inv(u64 a, u64 q);
+u64 host_to_mont(u64 x, u64 q);  // x * 2^64 mod q
 
 // NTT (ntt.hip)
 int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse);

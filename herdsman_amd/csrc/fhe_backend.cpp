@@ -31,7 +31,10 @@ static u64 hpow(u64 b, u64 e, u64 q) {
   return r;
 }
 static u64 hinv(u64 a, u64 q) { return hpow(a % q, q - 2, q); }
-static Tw htw(u64 w, u64 q) { return Tw{w, (u64)(((u128)w << 64) / q)}; }
+static u64 tomont(u64 x, u64 q) { return (u64)(((u128)(x % q) << 64) % q); }
+u64 host_mulmod(u64 a, u64 b, u64 q) { return hmul(a, b, q); }
+u64 host_inv(u64 a, u64 q) { return hinv(a, q); }
+u64 host_to_mont(u64 x, u64 q) { return tomont(x, q); }
 static u32 hbrv(u32 x, u32 bits) {
   u32 r = 0;
   for (u32 i = 0; i < bits; ++i) { r = (r << 1) | (x & 1); x >>= 1; }
@@ -59,11 +62,14 @@ static bool is_prime(u64 n) {
   }
   return true;
 }
-// largest primes q < 2^bits, q = 1 mod 2N, descending, not in `used`
-static bool gen_primes(u32 bits, u32 log_n, u32 count, std::vector<u64> &used, std::vector<u64> &out) {
-  const u64 two_n = 2ull << log_n;
-  for (u64 k = ((1ull << bits) - 2) / two_n; k > 0 && count; --k) {
-    const u64 q = k * two_n + 1;
+// Prime family of the backend: the largest primes q < 2^bits with
+// q = 1 (mod 2^32), descending, not in `used`.  q = 1 mod 2^32 implies
+// q = 1 mod 2N for every N <= 2^31 (NTT-friendly) and makes the Montgomery
+// quotient digit free on 32-bit multipliers (modarith.hpp).
+static bool gen_primes(u32 bits, u32 count, std::vector<u64> &used, std::vector<u64> &out) {
+  const u64 step = 1ull << 32;
+  for (u64 k = ((1ull << bits) - 2) / step; k > 0 && count; --k) {
+    const u64 q = k * step + 1;
     if (std::find(used.begin(), used.end(), q) != used.end()) continue;
     if (is_prime(q)) { out.push_back(q); used.push_back(q); --count; }
   }
@@ -123,29 +129,30 @@ int ctx_workspace(fhe_ctx *c, size_t bytes, void **out) {
   return FHE_OK;
 }
 
-ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst) {
+ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst, int r_exp) {
   ConvTab t{};
   t.ns = (u32)src.size();
   t.nd = (u32)dst.size();
-  std::vector<Tw> hi(t.ns);
+  std::vector<u64> hi(t.ns);
   std::vector<u64> h((size_t)t.ns * t.nd);
   for (u32 i = 0; i < t.ns; ++i) {
     const u64 si = c->moduli[src[i]];
     u64 prod = 1;
     for (u32 k = 0; k < t.ns; ++k)
       if (k != i) prod = hmul(prod, c->moduli[src[k]] % si, si);
-    hi[i] = htw(hinv(prod, si), si);
+    hi[i] = tomont(hinv(prod, si), si);
     for (u32 m = 0; m < t.nd; ++m) {
       const u64 dm = c->moduli[dst[m]];
       u64 p2 = 1;
       for (u32 k = 0; k < t.ns; ++k)
         if (k != i) p2 = hmul(p2, c->moduli[src[k]] % dm, dm);
+      for (int e = 0; e < r_exp; ++e) p2 = tomont(p2, dm);
       h[(size_t)i * t.nd + m] = p2;
     }
   }
   t.src_mod = (const u32 *)ctx_upload(c, src.data(), sizeof(u32) * t.ns);
   t.dst_mod = (const u32 *)ctx_upload(c, dst.data(), sizeof(u32) * std::max<u32>(t.nd, 1));
-  t.hinv = (const Tw *)ctx_upload(c, hi.data(), sizeof(Tw) * t.ns);
+  t.hinv = (const u64 *)ctx_upload(c, hi.data(), sizeof(u64) * t.ns);
   t.h = (const u64 *)ctx_upload(c, h.data(), sizeof(u64) * std::max<size_t>(h.size(), 1));
   return t;
 }
@@ -184,52 +191,60 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
     c->moduli.assign(p->moduli, p->moduli + c->nmod);
     const u64 two_n = 2ull << p->log_n;
     for (u64 q : c->moduli)
-      if (q >= (1ull << 62) || q % two_n != 1 || !is_prime(q))
-        return fhe_fail(c, FHE_ERR_INVALID, "explicit modulus is not an NTT-friendly prime < 2^62");
+      if (q >= (1ull << 61) || q % two_n != 1 || !is_prime(q))
+        return fhe_fail(c, FHE_ERR_INVALID, "explicit modulus is not an NTT-friendly prime < 2^61");
+    for (size_t i = 0; i < c->moduli.size(); ++i)
+      for (size_t j = 0; j < i; ++j)
+        if (c->moduli[i] == c->moduli[j]) return fhe_fail(c, FHE_ERR_INVALID, "duplicate modulus");
   } else {
-    if (p->q_bits < 20 || p->q_bits > 61 || p->p_bits < 20 || p->p_bits > 61)
-      return fhe_fail(c, FHE_ERR_INVALID, "q_bits / p_bits must be in [20, 61]");
+    if (p->q_bits < 36 || p->q_bits > 61 || p->p_bits < 36 || p->p_bits > 61)
+      return fhe_fail(c, FHE_ERR_INVALID, "q_bits / p_bits must be in [36, 61]");
     std::vector<u64> used;
-    if (!gen_primes(p->q_bits, p->log_n, c->L, used, c->moduli) ||
-        !gen_primes(p->p_bits, p->log_n, c->K, used, c->moduli) ||
-        !gen_primes(p->p_bits, p->log_n, c->nB, used, c->moduli))
-      return fhe_fail(c, FHE_ERR_INVALID, "not enough NTT-friendly primes");
+    if (!gen_primes(p->q_bits, c->L, used, c->moduli) || !gen_primes(p->p_bits, c->K, used, c->moduli) ||
+        !gen_primes(p->p_bits, c->nB, used, c->moduli))
+      return fhe_fail(c, FHE_ERR_INVALID, "not enough primes q = 1 mod 2^32 below the bit bound");
   }
+  c->special = true;
+  for (u64 q : c->moduli) c->special = c->special && ((q & 0xffffffffull) == 1);
   const u32 n = c->n, nm = c->nmod;
-  // per-modulus tables
+  // per-modulus tables, constants in Montgomery form (x * 2^64 mod q)
   std::vector<ModInfo> mods(nm);
-  std::vector<Tw> twf((size_t)nm * n), twi((size_t)nm * n), ninv(nm);
+  std::vector<u64> twf((size_t)nm * n), twi((size_t)nm * n), ninv(nm), r2(nm);
   std::vector<u64> pw(n), ipw(n);
   for (u32 m = 0; m < nm; ++m) {
     const u64 q = c->moduli[m];
-    const u128 mu = (~(u128)0) / q;
-    mods[m] = ModInfo{q, (u64)(mu >> 64), (u64)mu, 0};
+    u64 inv = q;  // q^-1 mod 2^64 by Newton iteration
+    for (int it = 0; it < 6; ++it) inv *= 2 - q * inv;
+    r2[m] = tomont(tomont(1, q), q);
+    mods[m] = ModInfo{q, 0 - inv, r2[m], (u32)(q >> 32), (u32)((q & 0xffffffffull) == 1)};
     const u64 psi = min_psi(q, c->log_n), ipsi = hinv(psi, q);
     u64 a = 1, b = 1;
     for (u32 i = 0; i < n; ++i) { pw[i] = a; ipw[i] = b; a = hmul(a, psi, q); b = hmul(b, ipsi, q); }
     for (u32 i = 0; i < n; ++i) {
       const u32 r = hbrv(i, c->log_n);
-      twf[(size_t)m * n + i] = htw(pw[r], q);
-      twi[(size_t)m * n + i] = htw(ipw[r], q);
+      twf[(size_t)m * n + i] = tomont(pw[r], q);
+      twi[(size_t)m * n + i] = tomont(ipw[r], q);
     }
-    ninv[m] = htw(hinv(n, q), q);
+    ninv[m] = tomont(hinv(n, q), q);
   }
   c->d_mods = (ModInfo *)ctx_upload(c, mods.data(), sizeof(ModInfo) * nm);
-  c->d_tw_fwd = (Tw *)ctx_upload(c, twf.data(), sizeof(Tw) * twf.size());
-  c->d_tw_inv = (Tw *)ctx_upload(c, twi.data(), sizeof(Tw) * twi.size());
-  c->d_ninv = (Tw *)ctx_upload(c, ninv.data(), sizeof(Tw) * nm);
-  if (!c->d_mods || !c->d_tw_fwd || !c->d_tw_inv || !c->d_ninv) return fhe_fail(c, FHE_ERR_OOM, "table upload");
+  c->d_tw_fwd = (u64 *)ctx_upload(c, twf.data(), sizeof(u64) * twf.size());
+  c->d_tw_inv = (u64 *)ctx_upload(c, twi.data(), sizeof(u64) * twi.size());
+  c->d_ninv = (u64 *)ctx_upload(c, ninv.data(), sizeof(u64) * nm);
+  c->d_r2 = (u64 *)ctx_upload(c, r2.data(), sizeof(u64) * nm);
+  if (!c->d_mods || !c->d_tw_fwd || !c->d_tw_inv || !c->d_ninv || !c->d_r2)
+    return fhe_fail(c, FHE_ERR_OOM, "table upload");
   // key-switching tables
   if (c->K) {
     const u32 L = c->L, QP = c->L + c->K;
-    std::vector<Tw> pinv(L);
+    std::vector<u64> pinv(L);
     for (u32 i = 0; i < L; ++i) {
       const u64 q = c->moduli[i];
       u64 P = 1;
       for (u32 k = 0; k < c->K; ++k) P = hmul(P, c->moduli[L + k] % q, q);
-      pinv[i] = htw(hinv(P, q), q);
+      pinv[i] = tomont(hinv(P, q), q);
     }
-    c->d_pinv = (Tw *)ctx_upload(c, pinv.data(), sizeof(Tw) * L);
+    c->d_pinv = (u64 *)ctx_upload(c, pinv.data(), sizeof(u64) * L);
     std::vector<ConvTab> tabs;
     for (u32 j = 0; j * c->alpha < L; ++j) {
       const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
@@ -237,13 +252,13 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
       for (u32 i = lo; i < hi; ++i) src.push_back(i);
       for (u32 i = 0; i < QP; ++i)
         if (i < lo || i >= hi) dst.push_back(i);
-      tabs.push_back(make_conv_tab(c, src, dst));
+      tabs.push_back(make_conv_tab(c, src, dst, 2));  // ModUp output carries a factor R
     }
     c->d_modup = (ConvTab *)ctx_upload(c, tabs.data(), sizeof(ConvTab) * tabs.size());
     std::vector<u32> src, dst;
     for (u32 k = 0; k < c->K; ++k) src.push_back(L + k);
     for (u32 i = 0; i < L; ++i) dst.push_back(i);
-    c->moddown = make_conv_tab(c, src, dst);
+    c->moddown = make_conv_tab(c, src, dst, 1);
     if (!c->d_pinv || !c->d_modup || !c->moddown.h) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
   }
   if (p->scheme == FHE_SCHEME_BFV) {
@@ -388,7 +403,7 @@ int fhe_base_conv(fhe_ctx *c, const uint64_t *src, const uint32_t *src_mods, uin
   auto it = cache.find({c, key});
   ConvTab t;
   if (it == cache.end()) {
-    t = make_conv_tab(c, s, d);
+    t = make_conv_tab(c, s, d, 1);
     if (!t.h) return fhe_fail(c, FHE_ERR_OOM, "conv table");
     cache[{c, key}] = t;
   } else {

@@ -1,14 +1,26 @@
 // modarith.hpp -- 64-bit modular arithmetic for gfx950 (device) and host.
 //
-// gfx950 has no 64x64 multiplier: a u64 product is emulated with 32-bit
-// v_mul_hi_u32 / v_mad_u64_u32, both quarter rate (measured:
-// tools/microbench/intops.hip, ~20 T lane-ops/s each).  A Shoup constant
-// multiply is ~10 such instructions; the backend therefore uses
-//   - Shoup multiplication for every constant operand (twiddles, CRT
-//     constants), lazy in [0, 2q);
-//   - 128-bit Barrett (mu = floor(2^128/q)) only for variable x variable
-//     products and for reducing lazily accumulated 128-bit dot products.
-// All moduli satisfy q < 2^62 so [0, 4q) lazy values fit a u64.
+// gfx950 has no 64x64 multiplier: every u64 product is built from 32-bit
+// v_mad_u64_u32 / v_mul_hi_u32 / v_mul_lo_u32, all QUARTER rate
+// (tools/microbench/intops.hip: ~20 T lane-ops/s each vs 78.6 T for a
+// full-rate VALU op).  The multiply count per modular product is therefore
+// the figure of merit, and the backend is built on Montgomery arithmetic with
+// R = 2^64:
+//   * mul128(a, b): the 128-bit product from exactly 4 v_mad_u64_u32;
+//   * mont_reduce(T) = T * 2^-64 mod q in [0, 2q) for T < q * 2^64:
+//       - "special" moduli q = 1 (mod 2^32) (the backend's default prime
+//         family, still NTT-friendly for every N <= 2^31): q' = -q^-1 = -1 mod
+//         2^32, so each of the two 32-bit Montgomery rounds needs ONE
+//         v_mad_u64_u32 (m * q_hi) -- 2 multiplies in total;
+//       - generic odd moduli (explicit OpenFHE-style primes): one 64-bit round
+//         with q' = -q^-1 mod 2^64, 7 multiplies;
+//   * every constant operand (twiddles, CRT constants, N^-1, P^-1) is stored
+//     pre-multiplied by R, so mont_mul(x, cR) = x * c exactly: a twiddle
+//     multiply costs 4 + 2 = 6 multiplies (Shoup needs 10);
+//   * dot products sum 128-bit products and reduce once; their constants are
+//     pre-scaled so the R^-1 of the single reduction cancels.
+// All moduli are < 2^61, so lazy values in [0, 4q) and the sums below stay
+// inside the Montgomery bound T < q * 2^64.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,14 +30,16 @@ typedef uint32_t u32;
 
 #define HD __host__ __device__ __forceinline__
 
-struct alignas(16) Tw {  // twiddle and its Shoup companion floor(w*2^64/q)
-  u64 w, ws;
-};
-
 struct ModInfo {
   u64 q;
-  u64 mu_hi, mu_lo;  // floor(2^128 / q)
-  u64 pad;
+  u64 qinv_neg;  // -q^-1 mod 2^64 (generic Montgomery)
+  u64 r2;        // R^2 mod q  (mont_mul(x, r2) = x * R)
+  u32 q_hi;      // q >> 32 (special Montgomery, q = q_hi * 2^32 + 1)
+  u32 special;   // q = 1 mod 2^32
+};
+
+struct U128 {
+  u64 lo, hi;
 };
 
 HD u64 mulhi64(u64 a, u64 b) {
@@ -36,58 +50,85 @@ HD u64 mulhi64(u64 a, u64 b) {
 #endif
 }
 
-// Shoup: a*w mod q for any a < 2^64; result in [0, 2q)
-HD u64 shoup_lazy(u64 a, u64 w, u64 ws, u64 q) {
-  u64 qh = mulhi64(a, ws);
-  return a * w - qh * q;
+// full 128-bit product from four 32x32->64 multiply-adds
+HD U128 mul128(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+  const u64 p00 = (u64)a0 * b0;
+  const u64 p01 = (u64)a0 * b1 + (p00 >> 32);
+  const u64 p10 = (u64)a1 * b0 + (u32)p01;
+  const u64 p11 = (u64)a1 * b1 + (p01 >> 32) + (p10 >> 32);
+  return U128{(p10 << 32) | (u32)p00, p11};
+#else
+  unsigned __int128 p = (unsigned __int128)a * b;
+  return U128{(u64)p, (u64)(p >> 64)};
+#endif
 }
-HD u64 shoup(u64 a, u64 w, u64 ws, u64 q) {
-  u64 r = shoup_lazy(a, w, ws, q);
-  return r >= q ? r - q : r;
-}
-HD u64 add_mod(u64 a, u64 b, u64 q) {
-  u64 s = a + b;
-  return s >= q ? s - q : s;
-}
-HD u64 sub_mod(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
-HD u64 csub(u64 a, u64 q) { return a >= q ? a - q : a; }
 
-// 128-bit accumulator
-struct U128 {
-  u64 lo, hi;
-};
-HD void mac128(U128 &acc, u64 a, u64 b) {
-  u64 lo = a * b, hi = mulhi64(a, b);
-  u64 s = acc.lo + lo;
-  acc.hi += hi + (s < lo);
+HD void add128(U128 &acc, const U128 &x) {
+  const u64 s = acc.lo + x.lo;
+  acc.hi += x.hi + (s < x.lo);
   acc.lo = s;
 }
-HD U128 mul128(u64 a, u64 b) {
-  U128 r;
-  r.lo = a * b;
-  r.hi = mulhi64(a, b);
-  return r;
+HD void mac128(U128 &acc, u64 a, u64 b) { add128(acc, mul128(a, b)); }
+
+// T * 2^-64 mod q, result in [0, 2q); requires T < q * 2^64.
+template <bool SP>
+HD u64 mont_reduce(U128 T, const ModInfo &m) {
+  if (SP) {
+    // round 1: t0 = T mod 2^32, mq = -t0, T1 = (T >> 32) + (t0 != 0) + mq * q_hi
+    const u32 t0 = (u32)T.lo;
+    const u64 M = (u64)(0u - t0) * m.q_hi + (t0 != 0);  // < 2^61
+    const u64 s = (T.hi << 32) | (T.lo >> 32);          // bits 32..95 of T
+    const u64 r = s + M;
+    const u32 top = (u32)(T.hi >> 32) + (r < s);        // bits 96..127 of T1
+    // round 2 on T1 = top:r
+    const u32 t1 = (u32)r;
+    const u64 M2 = (u64)(0u - t1) * m.q_hi + (t1 != 0);
+    return (((u64)top << 32) | (r >> 32)) + M2;
+  } else {
+    const u64 mm = T.lo * m.qinv_neg;
+    return T.hi + mulhi64(mm, m.q) + (T.lo != 0);
+  }
 }
 
-// Barrett reduction of x = hi*2^64 + lo, x < q*2^64, to [0, q).
-// qt = floor(x*mu / 2^128) with all carries kept, so qt in {Q*-1, Q*} and a
-// single conditional subtraction finishes.
-HD u64 barrett128(u64 hi, u64 lo, u64 q, u64 mu_hi, u64 mu_lo) {
-  u64 c = mulhi64(lo, mu_lo);
-  u64 t0 = lo * mu_hi, t1 = mulhi64(lo, mu_hi);
-  u64 s = t0 + c;
-  u64 s_hi = t1 + (s < t0);
-  u64 u0 = hi * mu_lo, u1 = mulhi64(hi, mu_lo);
-  u64 s2 = s + u0;
-  u64 carry = u1 + (s2 < s);
-  u64 qt = hi * mu_hi + s_hi + carry;
-  u64 r = lo - qt * q;
-  return r >= q ? r - q : r;
+// Special-modulus Montgomery product by word-serial CIOS: a < 2^63, b < q < 2^61,
+// q = q_hi * 2^32 + 1.  Six v_mad_u64_u32 and no 128-bit carry chains: the
+// bounds a_hi < 2^31 and b_hi < 2^29 keep every partial sum below 2^64.
+// Returns a*b*2^-64 mod q in [0, 1.5q).
+HD u64 mont_mul_sp(u64 a, u64 b, u32 q_hi) {
+  const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+  const u64 P = (u64)a0 * b0;
+  const u64 U = (u64)a1 * b0 + (P >> 32);            // t = U : P_lo
+  const u32 p0 = (u32)P;
+  const u64 V = (u64)(0u - p0) * q_hi + U + (p0 != 0);  // (t + m q) / 2^32
+  const u64 X0 = (u64)a0 * b1 + V;                   // t' = V + a b1 = X1 : x0
+  const u32 x0 = (u32)X0;
+  const u64 X1 = (u64)a1 * b1 + (X0 >> 32);
+  return (u64)(0u - x0) * q_hi + X1 + (x0 != 0);
 }
-HD u64 reduce128(U128 x, const ModInfo &m) { return barrett128(x.hi, x.lo, m.q, m.mu_hi, m.mu_lo); }
+
+template <bool SP>
+HD u64 mont_mul(u64 a, u64 b, const ModInfo &m) {  // a*b*2^-64, [0,2q); a < 2^63, b < q
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (SP) return mont_mul_sp(a, b, m.q_hi);
+#endif
+  return mont_reduce<SP>(mul128(a, b), m);
+}
+
+HD u64 csub(u64 a, u64 q) { return a >= q ? a - q : a; }
+HD u64 add_mod(u64 a, u64 b, u64 q) { return csub(a + b, q); }
+HD u64 sub_mod(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
+
+// exact a*b mod q (canonical) for variable operands: (a*b/R) * R^2 / R
+template <bool SP>
 HD u64 mul_mod(u64 a, u64 b, const ModInfo &m) {
-  U128 p = mul128(a, b);
-  return barrett128(p.hi, p.lo, m.q, m.mu_hi, m.mu_lo);
+  return csub(mont_mul<SP>(mont_reduce<SP>(mul128(a, b), m), m.r2, m), m.q);
+}
+// exact (T mod q) for a 128-bit T < q * 2^64
+template <bool SP>
+HD u64 reduce128(U128 T, const ModInfo &m) {
+  return csub(mont_mul<SP>(mont_reduce<SP>(T, m), m.r2, m), m.q);
 }
 
 // SplitMix64 stream shared with the oracle (orc_fill_uniform)

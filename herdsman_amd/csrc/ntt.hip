@@ -2,8 +2,10 @@
 //
 // Algorithm (same transform as the oracle's orc_ntt_fwd, oracle/fhe_oracle.c):
 // Harvey's lazy Cooley-Tukey forward (natural in, bit-reversed out, values in
-// [0,4q) between stages) and Gentleman-Sande inverse ([0,2q)), twiddle for the
-// butterfly (j, j+t) at global stage s is psi^brv(2^s + (j >> (logN - s))).
+// [0,4q) between stages) and Gentleman-Sande inverse ([0,2q)).  The twiddle of
+// butterfly (j, j+t) at global stage s is psi^brv(2^s + (j >> (logN - s))),
+// stored in Montgomery form (psi^e * 2^64 mod q) so one mont_mul = 6
+// quarter-rate multiplies gives the exact product (modarith.hpp).
 //
 // MI355X mapping.  One limb-polynomial of N u64 words is split into passes;
 // a pass owns global stages [s0, s0+S) and works on independent
@@ -15,17 +17,16 @@
 //               exceeds the 160 KiB LDS of a CU.
 // Inside a pass a workgroup holds W sub-transforms in LDS (coalesced 128 B
 // row segments in and out); each thread keeps R = 16 elements in VGPRs and
-// runs LOGR = 4 butterfly stages in registers between LDS exchanges, so LDS
-// traffic is 2 x S/4 round trips per element instead of one per stage.
+// runs LOGR = 4 butterfly stages in registers between LDS exchanges.
 #include "context.hpp"
 
 namespace {
 
 struct NttArgs {
   LimbMap map;
-  const Tw *tw;          // [nmod][N]
+  const u64 *tw;         // [nmod][N], Montgomery form
   const ModInfo *mods;   // [nmod]
-  const Tw *ninv;        // [nmod]
+  const u64 *ninv;       // [nmod], N^-1 in Montgomery form
   u32 log_n;
   u32 s0;                // first global stage of this pass
   u32 log_stride;        // sub-transform element stride = 2^log_stride
@@ -39,7 +40,7 @@ __device__ __forceinline__ u32 lds_idx(u32 w, u32 k) {
   return w * PAD + k + (k >> 4);
 }
 
-template <int S, int LOGR, int W, bool INV, bool COLS>
+template <int S, int LOGR, int W, bool INV, bool COLS, bool SP>
 __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   constexpr int R = 1 << LOGR;
   constexpr int T = 1 << (S - LOGR);
@@ -50,12 +51,14 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
 
   const u32 tid = threadIdx.x;
   const u32 e = blockIdx.y;
-  const u32 poly = e / a.map.cnt, act = e % a.map.cnt;
+  const u32 cnt = a.map.cnt;
+  const u32 poly = e / cnt, act = e - poly * cnt;
   const u32 limb = limbmap_limb(a.map, act);
   const u32 mod = a.map.mod_offset + limb;
   u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << a.log_n);
-  const u64 q = a.mods[mod].q, q2 = 2 * q;
-  const Tw *tw = a.tw + ((size_t)mod << a.log_n);
+  const ModInfo mi = a.mods[mod];
+  const u64 q = mi.q, q2 = 2 * q;
+  const u64 *tw = a.tw + ((size_t)mod << a.log_n);
   const u32 stride = 1u << a.log_stride;
 
   // ---- coalesced global -> LDS load of the W sub-transforms of this block
@@ -105,35 +108,30 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
         if (rb & half) continue;
         // top sigma bits of k for element r
         const u32 kk = ((((hh << ex) | rx) << tau) | (rb >> (nb - tau)));
-        const Tw t = tw[(1u << s) + (hi << sigma) + kk];
+        const u64 t = tw[(1u << s) + (hi << sigma) + kk];
         u64 &X = x[r];
         u64 &Y = x[r + half];
         if (!INV) {
-          u64 uu = X >= q2 ? X - q2 : X;
-          u64 v = shoup_lazy(Y, t.w, t.ws, q);
+          const u64 uu = X >= q2 ? X - q2 : X;
+          const u64 v = mont_mul<SP>(Y, t, mi);
           X = uu + v;
           Y = uu - v + q2;
         } else {
-          u64 uu = X, vv = Y;
-          u64 sm = uu + vv;
-          sm = sm >= q2 ? sm - q2 : sm;
-          X = sm;
-          Y = shoup_lazy(uu - vv + q2, t.w, t.ws, q);
+          const u64 uu = X, vv = Y;
+          const u64 sm = uu + vv;
+          X = sm >= q2 ? sm - q2 : sm;
+          Y = mont_mul<SP>(uu - vv + q2, t, mi);
         }
       }
     }
     if (gi == NG - 1 && a.last) {
       if (!INV) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          u64 v = x[r];
-          v = v >= q2 ? v - q2 : v;
-          x[r] = v >= q ? v - q : v;
-        }
+        for (int r = 0; r < R; ++r) x[r] = csub(csub(x[r], q2), q);
       } else {
-        const Tw sc = a.ninv[mod];
+        const u64 sc = a.ninv[mod];
 #pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = shoup(x[r], sc.w, sc.ws, q);
+        for (int r = 0; r < R; ++r) x[r] = csub(mont_mul<SP>(x[r], sc, mi), q);
       }
     }
 #pragma unroll
@@ -157,24 +155,25 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   }
 }
 
-template <int S, int W, bool COLS>
-int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+template <int S, int W, bool COLS, bool INV, bool SP>
+int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   constexpr int LOGR = 4;
   constexpr int NT = W << (S - LOGR);
   constexpr size_t SUB = 1u << S;
   constexpr size_t lds = (size_t)W * (SUB + (SUB >> 4) + 1) * sizeof(u64);
   const u32 subs = 1u << (a.log_n - S);
   dim3 grid(subs / W, n_jobs);
-  if (inv) {
-    auto k = ntt_pass<S, LOGR, W, true, COLS>;
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);
-  } else {
-    auto k = ntt_pass<S, LOGR, W, false, COLS>;
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);
-  }
+  auto k = ntt_pass<S, LOGR, W, INV, COLS, SP>;
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);
   return fhe_check(c, hipGetLastError(), "ntt_pass launch");
+}
+
+template <int S, int W, bool COLS>
+int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  if (c->special)
+    return inv ? launch_one<S, W, COLS, true, true>(c, a, n_jobs) : launch_one<S, W, COLS, false, true>(c, a, n_jobs);
+  return inv ? launch_one<S, W, COLS, true, false>(c, a, n_jobs) : launch_one<S, W, COLS, false, false>(c, a, n_jobs);
 }
 
 // one pass over a whole residue (N <= 2^14)

@@ -50,12 +50,14 @@ def is_prime(n: int) -> bool:
 
 
 def gen_primes(bits: int, log_n: int, count: int, exclude: Sequence[int] = ()) -> List[int]:
-    """Largest primes q < 2^bits with q = 1 mod 2N, descending."""
-    two_n = 2 << log_n
-    k = ((1 << bits) - 2) // two_n
+    """The backend's prime family: largest primes q < 2^bits with q = 1 mod 2^32
+    (which implies q = 1 mod 2N for N <= 2^31), descending."""
+    assert 2 << log_n <= 1 << 32
+    step = 1 << 32
+    k = ((1 << bits) - 2) // step
     out: List[int] = []
     while k > 0 and len(out) < count:
-        q = k * two_n + 1
+        q = k * step + 1
         if q not in exclude and is_prime(q):
             out.append(q)
         k -= 1

@@ -108,12 +108,14 @@ static int is_prime_u64(uint64_t n) {
 
 uint32_t orc_gen_primes(uint32_t bits, uint32_t log_n, uint32_t count, const uint64_t *excl,
                         uint32_t n_excl, uint64_t *out) {
-  /* q = k*2N + 1 < 2^bits, descending */
-  uint64_t two_n = 2ull << log_n;
-  uint64_t k = ((bits >= 64 ? ~0ull : (1ull << bits)) - 2) / two_n;
+  /* The backend's prime family: q = k * 2^32 + 1 < 2^bits, descending.
+   * q = 1 mod 2^32 implies q = 1 mod 2N for every N <= 2^31. */
+  (void)log_n;
+  const uint64_t step = 1ull << 32;
+  uint64_t k = ((bits >= 64 ? ~0ull : (1ull << bits)) - 2) / step;
   uint32_t got = 0;
   for (; k > 0 && got < count; --k) {
-    uint64_t q = k * two_n + 1;
+    uint64_t q = k * step + 1;
     int skip = 0;
     for (uint32_t e = 0; e < n_excl; ++e) if (excl[e] == q) skip = 1;
     for (uint32_t e = 0; e < got; ++e) if (out[e] == q) skip = 1;

@@ -52,7 +52,7 @@ void orc_ctx_destroy(orc_ctx *c);
 uint32_t orc_num_moduli(const orc_ctx *c);
 void orc_moduli(const orc_ctx *c, uint64_t *out);
 uint64_t orc_psi(const orc_ctx *c, uint32_t mod_idx);
-/* count primes q < 2^bits, q = 1 mod 2N, descending, skipping `excl` */
+/* count primes q < 2^bits, q = 1 mod 2^32 (hence mod 2N), descending, skipping `excl` */
 uint32_t orc_gen_primes(uint32_t bits, uint32_t log_n, uint32_t count,
                         const uint64_t *excl, uint32_t n_excl, uint64_t *out);
 void orc_set_threads(int n);

@@ -260,6 +260,51 @@ def test_bfv_real_keys_exact(hb):
     assert [((t * x + Qp // 2) // Qp) % t for x in v] == [x % t for x in automorph_int(m1, g)]
 
 
+# ------------------------------------------------- generic (non 2^32) moduli
+def _generic_primes(bits, log_n, count):
+    """q = 1 mod 2N but q != 1 mod 2^32: exercises the generic Montgomery path."""
+    import bigint_model as M
+    two_n = 2 << log_n
+    out, k = [], ((1 << bits) - 2) // two_n
+    while len(out) < count:
+        q = k * two_n + 1
+        if q % (1 << 32) != 1 and M.is_prime(q):
+            out.append(q)
+        k -= 1
+    return out
+
+
+def test_generic_moduli_ckks(hb):
+    log_n, L, K, dnum = 13, 4, 2, 2
+    mods = np.array(_generic_primes(60, log_n, L + K), dtype=np.uint64)
+    o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum, moduli=mods)
+    a = o.uniform((2, 2, L, 1 << log_n), seed=60)
+    b = o.uniform((2, 2, L, 1 << log_n), seed=61)
+    k = o.uniform(o.key_shape(), seed=62)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(k), dout)
+    assert np.array_equal(hb.to_host(dout), o.mul_relin(a, b, k))
+    g = o.galois_elt(2)
+    c.rotate(hb.to_device(a), g, hb.to_device(k), dout)
+    assert np.array_equal(hb.to_host(dout), o.rotate(a, g, k))
+
+
+def test_generic_moduli_ntt_and_bfv(hb):
+    log_n, L, K, dnum = 15, 3, 2, 2
+    mods = np.array(_generic_primes(60, log_n, 2 * L + K + 1), dtype=np.uint64)
+    o, c = pair(hb, SCHEME_BFV, log_n, L, K, dnum, t=65537, moduli=mods)
+    x = o.uniform((3, L, 1 << log_n), seed=70)
+    d = hb.to_device(x)
+    c.ntt_fwd(d)
+    assert np.array_equal(hb.to_host(d), o.ntt_fwd(x))
+    a = o.uniform((1, 2, L, 1 << log_n), seed=71)
+    b = o.uniform((1, 2, L, 1 << log_n), seed=72)
+    k = o.uniform(o.key_shape(), seed=73)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(k), dout)
+    assert np.array_equal(hb.to_host(dout), o.mul_relin(a, b, k))
+
+
 # ---------------------------------------------------------------- errors
 def test_errors_are_loud(hb):
     c = hb.Context(SCHEME_CKKS, 12, 2)
