@@ -108,6 +108,32 @@ HD u64 mont_mul_sp(u64 a, u64 b, u32 q_hi) {
   return (u64)(0u - x0) * q_hi + X1 + (x0 != 0);
 }
 
+// M independent mont_mul_sp products written phase by phase, so the
+// quarter-rate multiply chains of different products interleave in the
+// instruction stream instead of each serial chain stalling the wave.
+template <int M>
+HD void mont_mul_sp_vec(u64 (&r)[M], const u64 (&a)[M], const u64 (&b)[M], u32 q_hi) {
+  u64 t[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) t[i] = (u64)(u32)a[i] * (u32)b[i];                      // P
+#pragma unroll
+  for (int i = 0; i < M; ++i) r[i] = (u64)(u32)(a[i] >> 32) * (u32)b[i] + (t[i] >> 32);  // U
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const u32 p0 = (u32)t[i];
+    t[i] = (u64)(0u - p0) * q_hi + r[i] + (p0 != 0);                                   // V
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) t[i] = (u64)(u32)a[i] * (u32)(b[i] >> 32) + t[i];        // X0
+#pragma unroll
+  for (int i = 0; i < M; ++i) r[i] = (u64)(u32)(a[i] >> 32) * (u32)(b[i] >> 32) + (t[i] >> 32);  // X1
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const u32 x0 = (u32)t[i];
+    r[i] = (u64)(0u - x0) * q_hi + r[i] + (x0 != 0);
+  }
+}
+
 template <bool SP>
 HD u64 mont_mul(u64 a, u64 b, const ModInfo &m) {  // a*b*2^-64, [0,2q); a < 2^63, b < q
 #if defined(__HIP_DEVICE_COMPILE__)

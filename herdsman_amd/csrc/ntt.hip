@@ -10,14 +10,18 @@
 // MI355X mapping.  One limb-polynomial of N u64 words is split into passes;
 // a pass owns global stages [s0, s0+S) and works on independent
 // sub-transforms of 2^S elements at stride N >> (s0+S):
-//   N <= 2^14 : ONE pass, one residue per workgroup (2^14 x 8 B = 128 KiB in
+//   N <= 2^14 : ONE pass, one residue per workgroup (2^14 x 8 B = 128 KiB of
 //               LDS, 1024 threads) -- the north-star "one-residue-per-WG";
 //   N  = 2^15..2^17 : two passes (column pass of stride N/2^S1, then row pass
 //               of contiguous 2^S2 blocks), because a 512 KiB N=2^16 residue
 //               exceeds the 160 KiB LDS of a CU.
-// Inside a pass a workgroup holds W sub-transforms in LDS (coalesced 128 B
-// row segments in and out); each thread keeps R = 16 elements in VGPRs and
-// runs LOGR = 4 butterfly stages in registers between LDS exchanges.
+// Inside a pass each thread keeps R = 16 elements in VGPRs and runs LOGR = 4
+// butterfly stages in registers per "group"; groups are separated by ONE LDS
+// exchange (write, barrier, read).  The first group loads straight from HBM
+// and the last group stores straight to HBM (128 B row segments for column
+// passes, 16 contiguous words per lane for row passes), and each group's
+// twiddles are fetched while the previous group computes, so neither the
+// data nor the twiddle latency sits on the VALU critical path.
 #include "context.hpp"
 
 namespace {
@@ -40,13 +44,161 @@ __device__ __forceinline__ u32 lds_idx(u32 w, u32 k) {
   return w * PAD + k + (k >> 4);
 }
 
+// Group geometry (compile time): group g covers local stages
+// [g*LOGR, g*LOGR + nb); its butterfly bits are k bits [p, p+nb).  A thread
+// holds R = 2^LOGR elements k(r) = hh<<(p+nb+ex) | rx<<(p+nb) | rb<<p | lo_t.
+template <int S, int LOGR, int G>
+struct Grp {
+  static constexpr int nb = (S - G * LOGR) < LOGR ? (S - G * LOGR) : LOGR;
+  static constexpr int ex = LOGR - nb;
+  static constexpr int p = S - G * LOGR - nb;
+  static constexpr int NTW = (1 << ex) * ((1 << nb) - 1);  // distinct twiddles per thread
+  __device__ static __forceinline__ u32 k_of(int r, u32 ts) {
+    const u32 rb = r & ((1 << nb) - 1), rx = r >> nb;
+    return ((ts >> p) << (p + nb + ex)) | (rx << (p + nb)) | (rb << p) | (ts & ((1u << p) - 1));
+  }
+  // slot of (tau, rx, d) in the per-thread twiddle array, d < 2^tau
+  __device__ static constexpr int slot(int tau, int rx, int d) { return rx * ((1 << nb) - 1) + (1 << tau) - 1 + d; }
+  __device__ static __forceinline__ void load_tw(u64 (&t)[16], const u64 *tw, u32 s0, u32 hi, u32 ts) {
+    const u32 hh = ts >> p;
+#pragma unroll
+    for (int rx = 0; rx < (1 << ex); ++rx)
+#pragma unroll
+      for (int tau = 0; tau < nb; ++tau)
+#pragma unroll
+        for (int d = 0; d < (1 << tau); ++d) {
+          const u32 sigma = G * LOGR + tau;
+          const u32 kk = ((((hh << ex) | rx) << tau) | d);
+          t[slot(tau, rx, d)] = tw[(1u << (s0 + sigma)) + (hi << sigma) + kk];
+        }
+  }
+};
+
+template <int S, int LOGR, int G, bool INV, bool SP>
+__device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 q2, const ModInfo &mi) {
+  using GP = Grp<S, LOGR, G>;
+  constexpr int R = 1 << LOGR;
+#pragma unroll
+  for (int ti = 0; ti < GP::nb; ++ti) {
+    const int tau = INV ? GP::nb - 1 - ti : ti;
+    const int half = 1 << (GP::nb - 1 - tau);
+    if constexpr (SP) {
+      // the R/2 butterflies of this stage in lock-step (see mont_mul_sp_vec)
+      constexpr int H = R / 2;
+      u64 A[H], Wt[H], V[H], U[H];
+      int lo_idx[H];
+      {
+        int n = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int rb = r & ((1 << GP::nb) - 1), rx = r >> GP::nb;
+          if (rb & half) continue;
+          lo_idx[n] = r;
+          Wt[n] = t[GP::slot(tau, rx, rb >> (GP::nb - tau))];
+          ++n;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        const u64 X = x[lo_idx[i]], Y = x[lo_idx[i] + half];
+        if (!INV) {
+          U[i] = X >= q2 ? X - q2 : X;
+          A[i] = Y;
+        } else {
+          const u64 sm = X + Y;
+          U[i] = sm >= q2 ? sm - q2 : sm;
+          A[i] = X - Y + q2;
+        }
+      }
+      mont_mul_sp_vec<H>(V, A, Wt, mi.q_hi);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        if (!INV) {
+          x[lo_idx[i]] = U[i] + V[i];
+          x[lo_idx[i] + half] = U[i] - V[i] + q2;
+        } else {
+          x[lo_idx[i]] = U[i];
+          x[lo_idx[i] + half] = V[i];
+        }
+      }
+      continue;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int rb = r & ((1 << GP::nb) - 1), rx = r >> GP::nb;
+      if (rb & half) continue;
+      const u64 w = t[GP::slot(tau, rx, rb >> (GP::nb - tau))];
+      u64 &X = x[r];
+      u64 &Y = x[r + half];
+      if (!INV) {
+        const u64 uu = X >= q2 ? X - q2 : X;
+        const u64 v = mont_mul<SP>(Y, w, mi);
+        X = uu + v;
+        Y = uu - v + q2;
+      } else {
+        const u64 uu = X, vv = Y;
+        const u64 sm = uu + vv;
+        X = sm >= q2 ? sm - q2 : sm;
+        Y = mont_mul<SP>(uu - vv + q2, w, mi);
+      }
+    }
+  }
+}
+
+template <int S, int LOGR, int W, bool INV, bool COLS, bool SP, int GI>
+__device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds, const u64 *tw, u64 *data,
+                                           size_t gb, u32 stride, u32 w, u32 ts, u32 hi, const NttArgs &a,
+                                           const ModInfo &mi, u32 mod) {
+  constexpr int NG = (S + LOGR - 1) / LOGR;
+  constexpr int R = 1 << LOGR;
+  constexpr int G = INV ? NG - 1 - GI : GI;
+  using GP = Grp<S, LOGR, G>;
+  const u64 q = mi.q, q2 = 2 * q;
+  if constexpr (GI + 1 < NG) {
+    constexpr int GN = INV ? NG - 2 - GI : GI + 1;
+    u64 tn[16];
+    Grp<S, LOGR, GN>::load_tw(tn, tw, a.s0, hi, ts);  // in flight while this group computes
+    run_group<S, LOGR, G, INV, SP>(x, tc, q2, mi);
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, GP::k_of(r, ts))] = x[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lds[lds_idx<S>(w, Grp<S, LOGR, GN>::k_of(r, ts))];
+    group_loop<S, LOGR, W, INV, COLS, SP, GI + 1>(x, tn, lds, tw, data, gb, stride, w, ts, hi, a, mi, mod);
+  } else {
+    run_group<S, LOGR, G, INV, SP>(x, tc, q2, mi);
+    if (a.last) {
+      if (!INV) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = csub(csub(x[r], q2), q);
+      } else {
+        const u64 sc = a.ninv[mod];
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = csub(mont_mul<SP>(x[r], sc, mi), q);
+      }
+    }
+    if constexpr (!COLS && G != 0) {
+      // row pass ending in a group whose lanes each own contiguous words:
+      // re-layout through LDS so the HBM store is coalesced (group-0 layout)
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, GP::k_of(r, ts))] = x[r];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        data[gb + Grp<S, LOGR, 0>::k_of(r, ts)] = lds[lds_idx<S>(w, Grp<S, LOGR, 0>::k_of(r, ts))];
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) data[gb + (size_t)GP::k_of(r, ts) * stride] = x[r];
+    }
+  }
+}
+
 template <int S, int LOGR, int W, bool INV, bool COLS, bool SP>
 __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   constexpr int R = 1 << LOGR;
   constexpr int T = 1 << (S - LOGR);
-  constexpr int NT = W * T;
   constexpr int NG = (S + LOGR - 1) / LOGR;
-  constexpr int SUB = 1 << S;
+  static_assert(R == 16, "register tile is 16 words");
   extern __shared__ u64 lds[];
 
   const u32 tid = threadIdx.x;
@@ -57,102 +209,36 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   const u32 mod = a.map.mod_offset + limb;
   u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << a.log_n);
   const ModInfo mi = a.mods[mod];
-  const u64 q = mi.q, q2 = 2 * q;
   const u64 *tw = a.tw + ((size_t)mod << a.log_n);
   const u32 stride = 1u << a.log_stride;
 
-  // ---- coalesced global -> LDS load of the W sub-transforms of this block
-  // element (w, k) of the tile = data[hi * 2^(S+ls) + k * stride + lo] with
-  // sub-transform u = blockIdx.x * W + w, hi = u >> ls, lo = u & (stride-1)
-#pragma unroll 4
-  for (u32 idx = tid; idx < (u32)(W * SUB); idx += NT) {
-    u32 w, k;
-    if (COLS) { w = idx % W; k = idx / W; } else { w = idx / SUB; k = idx % SUB; }
-    const u32 u = blockIdx.x * W + w;
-    const size_t j = ((size_t)(u >> a.log_stride) << (S + a.log_stride)) + (size_t)k * stride +
-                     (u & (stride - 1));
-    lds[lds_idx<S>(w, k)] = data[j];
-  }
-  __syncthreads();
-
+  // column passes put the W sub-transforms (adjacent columns) on adjacent
+  // lanes: every wave access is four 128 B row segments
   u32 w, ts;
   if (COLS) { w = tid % W; ts = tid / W; } else { ts = tid % T; w = tid / T; }
   const u32 u = blockIdx.x * W + w;
   const u32 hi = u >> a.log_stride;
+  const size_t gb = ((size_t)hi << (S + a.log_stride)) + (u & (stride - 1));
 
+  constexpr int G0 = INV ? NG - 1 : 0;
+  u64 tc[16];
+  Grp<S, LOGR, G0>::load_tw(tc, tw, a.s0, hi, ts);
   u64 x[R];
+  if constexpr (!COLS && G0 != 0) {
+    // row pass starting in a per-lane-contiguous group: coalesced load in the
+    // group-0 layout, then one LDS re-layout
 #pragma unroll
-  for (int gi = 0; gi < NG; ++gi) {
-    const int g = INV ? NG - 1 - gi : gi;
-    const int nb = (S - g * LOGR) < LOGR ? (S - g * LOGR) : LOGR;   // butterfly bits
-    const int ex = LOGR - nb;                                      // extra register bits
-    const int p = S - g * LOGR - nb;                               // lowest butterfly bit
-    const u32 lo_t = ts & ((1u << p) - 1);
-    const u32 hh = ts >> p;
-    // k(r) = (hh << (p+nb+ex)) | (r_x << (p+nb)) | (r_b << p) | lo_t, r = (r_x << nb) | r_b
+    for (int r = 0; r < R; ++r) x[r] = data[gb + Grp<S, LOGR, 0>::k_of(r, ts)];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const u32 rb = r & ((1 << nb) - 1), rx = r >> nb;
-      const u32 k = (hh << (p + nb + ex)) | (rx << (p + nb)) | (rb << p) | lo_t;
-      x[r] = lds[lds_idx<S>(w, k)];
-    }
-#pragma unroll
-    for (int ti = 0; ti < nb; ++ti) {
-      const int tau = INV ? nb - 1 - ti : ti;
-      const u32 sigma = g * LOGR + tau;
-      const u32 s = a.s0 + sigma;
-      const int half = 1 << (nb - 1 - tau);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const u32 rb = r & ((1 << nb) - 1), rx = r >> nb;
-        if (rb & half) continue;
-        // top sigma bits of k for element r
-        const u32 kk = ((((hh << ex) | rx) << tau) | (rb >> (nb - tau)));
-        const u64 t = tw[(1u << s) + (hi << sigma) + kk];
-        u64 &X = x[r];
-        u64 &Y = x[r + half];
-        if (!INV) {
-          const u64 uu = X >= q2 ? X - q2 : X;
-          const u64 v = mont_mul<SP>(Y, t, mi);
-          X = uu + v;
-          Y = uu - v + q2;
-        } else {
-          const u64 uu = X, vv = Y;
-          const u64 sm = uu + vv;
-          X = sm >= q2 ? sm - q2 : sm;
-          Y = mont_mul<SP>(uu - vv + q2, t, mi);
-        }
-      }
-    }
-    if (gi == NG - 1 && a.last) {
-      if (!INV) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = csub(csub(x[r], q2), q);
-      } else {
-        const u64 sc = a.ninv[mod];
-#pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = csub(mont_mul<SP>(x[r], sc, mi), q);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const u32 rb = r & ((1 << nb) - 1), rx = r >> nb;
-      const u32 k = (hh << (p + nb + ex)) | (rx << (p + nb)) | (rb << p) | lo_t;
-      lds[lds_idx<S>(w, k)] = x[r];
-    }
+    for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, Grp<S, LOGR, 0>::k_of(r, ts))] = x[r];
     __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lds[lds_idx<S>(w, Grp<S, LOGR, G0>::k_of(r, ts))];
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = data[gb + (size_t)Grp<S, LOGR, G0>::k_of(r, ts) * stride];
   }
-
-  // ---- LDS -> global, coalesced
-#pragma unroll 4
-  for (u32 idx = tid; idx < (u32)(W * SUB); idx += NT) {
-    u32 w2, k;
-    if (COLS) { w2 = idx % W; k = idx / W; } else { w2 = idx / SUB; k = idx % SUB; }
-    const u32 u2 = blockIdx.x * W + w2;
-    const size_t j = ((size_t)(u2 >> a.log_stride) << (S + a.log_stride)) + (size_t)k * stride +
-                     (u2 & (stride - 1));
-    data[j] = lds[lds_idx<S>(w2, k)];
-  }
+  group_loop<S, LOGR, W, INV, COLS, SP, 0>(x, tc, lds, tw, data, gb, stride, w, ts, hi, a, mi, mod);
 }
 
 template <int S, int W, bool COLS, bool INV, bool SP>
