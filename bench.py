@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline duration")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the timed NTT loop (for rocprofv3 runs of the dominant kernel)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "ntt_traffic.json"))
     return ap.parse_args()
 
@@ -92,14 +94,15 @@ def main():
     def step():
         ctx.mul_relin(a, b, rlk, out)
 
-    for _ in range(args.warmup):
+    steps = 0 if args.roofline_only else args.steps
+    for _ in range(0 if args.roofline_only else args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -110,8 +113,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total = world * B * args.steps
-    value = total / elapsed
+    total = world * B * steps
+    value = total / elapsed if steps else 0.0
 
     # ---- dominant kernel group: forward NTT over the ModUp-sized batch (36 limbs per ct)
     limbs = B * 3 * L  # the converted limbs of one batch's ModUp
@@ -151,7 +154,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(elapsed / max(steps, 1) * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -1,0 +1,66 @@
+"""Turn a tools/profile_round.sh output dir into committed evidence under profiles/<round>/.
+
+    python tools/collect_profile.py gpurun_out/prof profiles/r01
+
+Writes <round>/roofline_kernel_stats.csv, bench_kernel_stats.csv, ntt_pmc.csv,
+summary.json and profiles/ntt_traffic.json (read by bench.py for roofline.traffic).
+HBM bytes follow MI355X_MICROARCH.md: FETCH_SIZE (KB) x 1024 x 2 (gfx950 reports
+half of a wide streaming read), WRITE_SIZE (KB) x 1024 as is.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+
+LOG_N, L = 16, 12
+
+
+def short(name):
+    m = re.search(r"(\w+)<([^()]*)>", name)
+    return f"{m.group(1)}<{m.group(2)}>" if m else name.split("(")[0]
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    for tag in ("roofline", "bench"):
+        f = glob.glob(f"{src}/{tag}/*kernel_stats.csv")
+        if f:
+            shutil.copy(f[0], f"{dst}/{tag}_kernel_stats.csv")
+    stats = list(csv.DictReader(open(f"{dst}/roofline_kernel_stats.csv")))
+    ntt = {short(r["Name"]): float(r["AverageNs"]) for r in stats if "ntt_pass" in r["Name"]}
+    launch_ns = sum(ntt.values())
+    rows, fetch, write = [], {}, {}
+    for tag, store in (("pmc_fetch", fetch), ("pmc_write", write)):
+        for f in glob.glob(f"{src}/{tag}/*counter_collection.csv"):
+            for r in csv.DictReader(open(f)):
+                if "ntt_pass" not in r["Kernel_Name"]:
+                    continue
+                k = short(r["Kernel_Name"])
+                store.setdefault(k, []).append(float(r["Counter_Value"]))
+                rows.append({"kernel": k, "counter": r["Counter_Name"], "value": r["Counter_Value"],
+                             "grid": r["Grid_Size"]})
+    with open(f"{dst}/ntt_pmc.csv", "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=["kernel", "counter", "value", "grid"])
+        w.writeheader()
+        w.writerows(rows)
+    fetch_b = sum(sum(v) / len(v) for v in fetch.values()) * 1024 * 2
+    write_b = sum(sum(v) / len(v) for v in write.values()) * 1024
+    # bench.py --roofline-only: 32 ciphertexts x 3 digits x 12 limbs per fhe_ntt_fwd launch
+    limbs = 32 * 3 * L
+    per_limb = (fetch_b + write_b) / limbs
+    summary = {"ntt_pass_avg_ns": ntt, "ntt_fwd_launch_ns": launch_ns, "limbs_per_launch": limbs,
+               "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+               "hbm_bytes_per_limb_ntt": per_limb,
+               "algorithmic_bytes_per_limb_ntt": 2 * (1 << LOG_N) * 8,
+               "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half of a wide stream read)"}
+    json.dump(summary, open(f"{dst}/summary.json", "w"), indent=1)
+    json.dump({"hbm_bytes_per_limb_ntt": per_limb, "source": dst}, open(os.path.join(os.path.dirname(dst),
+              "ntt_traffic.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
