@@ -58,10 +58,10 @@ def main():
     import torch.distributed as dist
 
     import herdsman_amd.backend as hb
+    from herdsman_amd.dist import broadcast_key, max_over_ranks
+    from herdsman_amd.dist import world as dist_world
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, local, world = dist_world()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -80,8 +80,7 @@ def main():
         ctx.fill_uniform(rlk, seed=0x524C4B)
     torch.cuda.synchronize(dev)
     t_b = time.perf_counter()
-    if world > 1:
-        dist.broadcast(rlk, src=0)
+    broadcast_key(rlk, src=0)  # the only collective: RCCL over xGMI
     torch.cuda.synchronize(dev)
     key_bcast_ms = (time.perf_counter() - t_b) * 1e3
 
@@ -108,11 +107,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
     total = world * B * steps
     value = total / elapsed if steps else 0.0
 

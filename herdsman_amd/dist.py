@@ -1,0 +1,47 @@
+"""Multi-GPU plumbing for the ciphertext-batch path.
+
+One process per GPU.  Ciphertexts are independent, so a batch shards with no
+data-path collective; the only collective is ONE broadcast of the evaluation
+key from rank 0 (RCCL over xGMI when the backend is "nccl").  This mirrors
+herdsman's own partition sharding (/root/reference/src/service/
+execution_service.cpp:545-548: one task per partition; partition p holds
+floor(rows/P) rows, +1 for p < rows mod P, storage_service.cpp:121-129).
+"""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+
+def world() -> Tuple[int, int, int]:
+    """(rank, local_rank, world_size) from the torchrun environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def shard_range(total: int, world_size: int, rank: int) -> Tuple[int, int]:
+    """[begin, end) of `rank`'s items: floor(total/W) each, +1 for rank < total mod W
+    (the same rule herdsman uses to split rows over partitions)."""
+    if world_size <= 0 or not 0 <= rank < world_size:
+        raise ValueError("bad rank / world size")
+    base, extra = divmod(total, world_size)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def broadcast_key(key, src: int = 0) -> None:
+    """Broadcast an evaluation key tensor in place (the only collective)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(key, src=src)
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    """Max of a host float over ranks (timing: the job ends when the slowest rank ends)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

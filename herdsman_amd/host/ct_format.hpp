@@ -1,0 +1,57 @@
+// ct_format.hpp -- on-disk formats the GPU worker group reads and writes.
+//
+// herdsman stores client data as opaque rows and keys as opaque blobs:
+//   * partition file <storage>/<session>/<frame>/<partition> = sequence of
+//     rows, each `uint32 length` + payload        (/root/reference/src/service/storage_service.cpp:19-28,233-240)
+//   * key file <key_dir>/<session>/<int(schema)>.key, written verbatim
+//                                                  (/root/reference/src/service/key_service.cpp:19-44)
+// Their payload encoding (presumably OpenFHE serialisation) is not pinned by
+// anything in the tree, so this backend defines its own, documented in
+// INTEGRATION.md:
+//   row payload   = 1..k ciphertexts, each: CtHeader + 2*L*N u64 words
+//   key file      = KeyFileHeader + n_keys x (KeyEntryHeader + dnum*2*(L+K)*N u64)
+// All integers little-endian.
+#pragma once
+#include <cstdint>
+#include <filesystem>
+#include <string>
+#include <vector>
+
+namespace herdsman_gpu {
+
+constexpr uint32_t kCtMagic = 0x54434648;   // "HFCT"
+constexpr uint32_t kKeyMagic = 0x424B4648;  // "HFKB"
+
+struct CtHeader {
+  uint32_t magic = kCtMagic;
+  uint16_t version = 1;
+  uint8_t scheme = 0;   // 0 CKKS, 1 BFV
+  uint8_t domain = 0;   // 1 = NTT (CKKS), 0 = coefficient (BFV)
+  uint32_t log_n = 0;
+  uint32_t n_limbs = 0; // L
+  uint64_t moduli_digest = 0;  // FNV-1a of the Q moduli, guards against parameter mix-ups
+};
+static_assert(sizeof(CtHeader) == 24, "CtHeader layout");
+
+struct KeyFileHeader {
+  uint32_t magic = kKeyMagic;
+  uint16_t version = 1;
+  uint8_t scheme = 0;
+  uint8_t pad = 0;
+  uint32_t log_n = 0, L = 0, K = 0, dnum = 0, n_keys = 0, pad2 = 0;
+  uint64_t moduli_digest = 0;  // FNV-1a of Q u P
+};
+static_assert(sizeof(KeyFileHeader) == 40, "KeyFileHeader layout");
+
+struct KeyEntryHeader {
+  uint32_t kind = 0;        // 0 = relinearisation, 1 = Galois
+  uint32_t galois_elt = 0;  // for kind 1
+};
+
+uint64_t moduli_digest(const uint64_t *moduli, uint32_t count);
+
+// rows of a partition file (payload bytes only)
+std::vector<std::vector<uint8_t>> read_partition(const std::filesystem::path &path);
+void write_partition(const std::filesystem::path &path, const std::vector<std::vector<uint8_t>> &rows);
+
+}  // namespace herdsman_gpu

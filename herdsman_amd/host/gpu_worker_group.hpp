@@ -1,0 +1,119 @@
+// gpu_worker_group.hpp -- in-process, MI355X-backed IWorkerGroup for herdsman.
+//
+// Replaces the remote-worker transports (GrpcWorkerGroup, LambdaWorkerGroup;
+// /root/reference/src/execution/worker/grpc/grpc_worker_group.cpp:70-105) with
+// a group that evaluates MapTask / ReduceTask circuits on local GPUs through
+// the C ABI of include/plugins/fhe_backend.h.  The Executor
+// (/root/reference/src/execution/executor/executor.cpp:82-113) and the
+// service layer are unchanged: they see the same schedule_task /
+// concurrent_workers / TaskHandle contract.
+//
+// Contract kept:
+//   * schedule_task never blocks on GPU work: it enqueues and returns;
+//   * one worker thread + one fhe_ctx per (device, schema) does the work,
+//     all rows of a partition in batched GPU calls;
+//   * no exception crosses the seam: failures become Status::ERROR;
+//   * the handle stays alive in the group until its completion is delivered;
+//   * completion is delivered on the group's own completion thread, and is
+//     re-tried until the executor's callback is attached: the executor sets
+//     the callback only AFTER schedule_task returns (executor.cpp:86-93) and
+//     TaskHandle::mark_completed silently drops a completion with no callback
+//     (i_worker_group.cpp:9-12).  The handle detects delivery because the base
+//     mark_completed evaluates the virtual status() exactly when it invokes
+//     the callback.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <filesystem>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/plugins/fhe_backend.h"
+#include "herd_seam.hpp"
+
+namespace herdsman_gpu {
+
+struct SchemaParams {
+  int schema_type = 0;
+  fhe_params params{};
+  std::vector<uint64_t> moduli;  // optional explicit moduli (copied into params.moduli)
+};
+
+// BASELINE.json parameter sets keyed by herdsman schema_type (herd_common's
+// SchemaType values are not in the snapshot; 0 = CKKS, 1 = BFV here).
+inline std::vector<SchemaParams> default_schemas() {
+  SchemaParams ckks, bfv;
+  ckks.schema_type = 0;
+  ckks.params = fhe_params{FHE_SCHEME_CKKS, 16, 12, 4, 3, 60, 61, 0, 0, nullptr};
+  bfv.schema_type = 1;
+  bfv.params = fhe_params{FHE_SCHEME_BFV, 15, 8, 4, 2, 60, 61, 0, 65537, nullptr};
+  return {ckks, bfv};
+}
+
+struct GpuWorkerGroupConfig {
+  std::vector<int> devices{0};
+  std::filesystem::path storage_dir;  // <storage>/<session>/<frame>/<partition>
+  std::filesystem::path key_dir;      // <key_dir>/<session>/<schema>.key
+  std::vector<SchemaParams> schemas;
+  uint32_t tasks_per_device = 2;      // concurrent_workers() = devices * tasks_per_device
+  uint32_t max_batch = 64;            // rows per batched GPU call
+};
+
+class GpuWorkerGroup : public IWorkerGroup {
+ public:
+  explicit GpuWorkerGroup(GpuWorkerGroupConfig config);
+  ~GpuWorkerGroup() override;
+
+  std::shared_ptr<TaskHandle> schedule_task(const herd::common::task_t &task) override;
+  std::size_t concurrent_workers() const noexcept override;
+
+  class Handle;
+
+ private:
+  struct Job {
+    std::shared_ptr<Handle> handle;
+    herd::common::task_t task;
+  };
+  struct Device;
+
+  void device_loop(Device &dev);
+  void completion_loop();
+  void complete(const std::shared_ptr<Handle> &h, TaskHandle::Status st);
+
+  GpuWorkerGroupConfig config_;
+  std::vector<std::unique_ptr<Device>> devices_;
+  std::atomic<size_t> next_device_{0};
+
+  std::mutex done_mutex_;
+  std::condition_variable done_cv_;
+  std::deque<std::shared_ptr<Handle>> done_;
+  bool stopping_ = false;
+  std::thread completion_thread_;
+};
+
+class GpuWorkerGroup::Handle : public IWorkerGroup::TaskHandle {
+ public:
+  Status status() const noexcept override {
+    if (probing_.load()) probed_.store(true);
+    return status_.load();
+  }
+  // completion thread only: true once the executor's callback has run
+  bool try_deliver() {
+    probed_.store(false);
+    probing_.store(true);
+    mark_completed();
+    probing_.store(false);
+    return probed_.load();
+  }
+  std::atomic<Status> status_{Status::PENDING};
+
+ private:
+  mutable std::atomic<bool> probing_{false};
+  mutable std::atomic<bool> probed_{false};
+};
+
+}  // namespace herdsman_gpu

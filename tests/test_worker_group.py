@@ -1,0 +1,169 @@
+"""The IWorkerGroup adaptor (herdsman_amd/host/gpu_worker_group.cpp) driven the
+way herdsman's Executor drives a worker group (schedule_task, then
+set_completion_callback; /root/reference/src/execution/executor/executor.cpp:82-94).
+
+CPU tests: the completion hand-off never loses a task even when the task
+finishes before the callback is attached, and a task on a machine without a
+GPU fails loudly (Status::ERROR), never on a CPU fallback.
+GPU tests: MapTask / ReduceTask end to end over herdsman's partition-file
+layout (<storage>/<session>/<frame>/<partition>, rows = u32 length + payload,
+storage_service.cpp:19-28,233-240) and key-file layout
+(<key_dir>/<session>/<schema>.key, key_service.cpp:28-31), bit-exact vs the
+CPU oracle.
+"""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WG_RUN = os.path.join(ROOT, "herdsman_amd", "bin", "wg_run")
+
+
+@pytest.fixture(scope="module")
+def wg_run():
+    if not os.path.exists(WG_RUN):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "herdsman_amd"), "host"], check=True)
+    return WG_RUN
+
+
+# ------------------------------------------------------------- formats
+def fnv(moduli):
+    h = 0xcbf29ce484222325
+    for q in moduli:
+        for b in range(8):
+            h ^= (int(q) >> (8 * b)) & 0xff
+            h = (h * 0x100000001b3) & (2**64 - 1)
+    return h
+
+
+def ct_row(o, cts):
+    """row payload: concatenated (CtHeader + words) ciphertexts."""
+    out = b""
+    for ct in cts:
+        hdr = struct.pack("<IHBBIIQ", 0x54434648, 1, o.scheme, 1 if o.scheme == 0 else 0, o.log_n, o.L,
+                          fnv(o.moduli[:o.L]))
+        out += hdr + np.ascontiguousarray(ct, dtype=np.uint64).tobytes()
+    return out
+
+
+def parse_row(o, payload):
+    assert struct.unpack_from("<I", payload)[0] == 0x54434648
+    return np.frombuffer(payload[24:], dtype=np.uint64).reshape(2, o.L, o.n)
+
+
+def write_partition(path, rows):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "wb") as f:
+        for r in rows:
+            f.write(struct.pack("<I", len(r)) + r)
+
+
+def read_partition(path):
+    data, rows, off = open(path, "rb").read(), [], 0
+    while off < len(data):
+        (n,) = struct.unpack_from("<I", data, off)
+        rows.append(data[off + 4:off + 4 + n])
+        off += 4 + n
+    return rows
+
+
+def write_keys(path, o, relin, galois):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHBBIIIIIIQ", 0x424B4648, 1, o.scheme, 0, o.log_n, o.L, o.K, o.dnum,
+                            1 + len(galois), 0, fnv(o.moduli[:o.L + o.K])))
+        f.write(struct.pack("<II", 0, 0) + np.ascontiguousarray(relin).tobytes())
+        for g, k in galois.items():
+            f.write(struct.pack("<II", 1, g) + np.ascontiguousarray(k).tobytes())
+
+
+def params_arg(o, tmp):
+    mf = os.path.join(tmp, "moduli.txt")
+    with open(mf, "w") as f:
+        f.write("\n".join(str(int(q)) for q in o.moduli))
+    return f"{o.scheme},{o.log_n},{o.L},{o.K},{o.dnum},{o.t},{mf}"
+
+
+# ---------------------------------------------------------------- CPU
+def test_completion_handoff_never_loses_a_task(wg_run):
+    r = subprocess.run([wg_run, "race", "200"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "200/200 delivered" in r.stdout
+
+
+def test_no_gpu_task_fails_loudly(wg_run, tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    r = subprocess.run([wg_run, "map", str(tmp_path), str(tmp_path), "s", "0", "0,12,2,1,1,0", "in", "0", "out",
+                        "in0", "in0", "add"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "status: ERROR" in r.stdout
+
+
+# ---------------------------------------------------------------- GPU
+def _setup(tmp_path, scheme, log_n, L, K, dnum, t=0):
+    from oracle_ffi import Oracle
+    o = Oracle(scheme, log_n, L, K, dnum, t=t)
+    return o, str(tmp_path / "storage"), str(tmp_path / "keys")
+
+
+@pytest.mark.gpu
+def test_gpu_map_task_mul_rotate(wg_run, tmp_path):
+    from oracle_ffi import SCHEME_CKKS
+    o, storage, keys = _setup(tmp_path, SCHEME_CKKS, 12, 4, 2, 2)
+    rows = 5
+    a = o.uniform((rows, 2, o.L, o.n), seed=1)
+    b = o.uniform((rows, 2, o.L, o.n), seed=2)
+    rlk = o.uniform(o.key_shape(), seed=3)
+    g = o.galois_elt(3)
+    gk = o.uniform(o.key_shape(), seed=4)
+    write_partition(os.path.join(storage, "sess", "frameA", "2"), [ct_row(o, [a[i], b[i]]) for i in range(rows)])
+    write_keys(os.path.join(keys, "sess", "7.key"), o, rlk, {g: gk})
+    r = subprocess.run([wg_run, "map", storage, keys, "sess", "7", params_arg(o, str(tmp_path)), "frameA", "2",
+                        "frameB", "in0", "in1", "mul", "rot:3"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.stack([parse_row(o, p) for p in read_partition(os.path.join(storage, "sess", "frameB", "2"))])
+    want = o.rotate(o.mul_relin(a, b, rlk), g, gk)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_reduce_task_add_and_mul_trees(wg_run, tmp_path):
+    from oracle_ffi import SCHEME_BFV
+    o, storage, keys = _setup(tmp_path, SCHEME_BFV, 12, 3, 3, 1, t=65537)
+    parts = {"p0": 3, "p1": 1, "p2": 3}
+    cts, i = [], 0
+    for name, cnt in parts.items():
+        rows = []
+        for _ in range(cnt):
+            ct = o.uniform((1, 2, o.L, o.n), seed=100 + i)[0]
+            cts.append(ct)
+            rows.append(ct_row(o, [ct]))
+            i += 1
+        write_partition(os.path.join(storage, "s2", name, "0"), rows)
+    rlk = o.uniform(o.key_shape(), seed=9)
+    write_keys(os.path.join(keys, "s2", "1.key"), o, rlk, {})
+    inputs = [f"{n}:0" for n in parts]
+    args = [wg_run, "reduce", storage, keys, "s2", "1", params_arg(o, str(tmp_path))]
+    r = subprocess.run(args + ["outA", "0"] + inputs, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = parse_row(o, read_partition(os.path.join(storage, "s2", "outA", "0"))[0])
+    want = cts[0]
+    for c in cts[1:]:
+        want = o.ct_add(want[None], c[None])[0]
+    assert np.array_equal(got, want)
+    # multiplicative tree: replicate the group's level order exactly
+    r = subprocess.run(args + ["outM", "0"] + inputs + ["--", "mul"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = parse_row(o, read_partition(os.path.join(storage, "s2", "outM", "0"))[0])
+    live = [c for c in cts]
+    while len(live) > 1:
+        half = len(live) // 2
+        lo = np.stack(live[:half])
+        hi = np.stack(live[len(live) - half:])
+        comb = o.mul_relin(lo, hi, rlk)
+        live = list(comb) + live[half:len(live) - half]
+    assert np.array_equal(got, live[0])
