@@ -440,12 +440,7 @@ int fhe_mul_relin(fhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64
   if (!b) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   if (!n_ct) return FHE_OK;
   if (c->params.scheme == FHE_SCHEME_BFV) return bfv_mul_relin_impl(c, a, b, rlk, out, n_ct);
-  const size_t LN = (size_t)c->L * c->n;
-  void *ws;
-  if ((rc = ctx_workspace(c, sizeof(u64) * n_ct * LN + keyswitch_ws_bytes(c, n_ct), &ws))) return rc;
-  u64 *d2 = (u64 *)ws;
-  if ((rc = tensor_launch(c, a, 2 * LN, LN, b, 2 * LN, LN, out, 2 * LN, LN, d2, LN, n_ct, c->L, 0))) return rc;
-  return keyswitch_ex(c, d2, c->L, rlk, out, out, n_ct, 3u, true, d2 + n_ct * LN);
+  return ckks_mul_relin_impl(c, a, b, rlk, out, n_ct);
 }
 
 int fhe_keyswitch(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n) {
@@ -462,13 +457,7 @@ int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, u
   if (rc) return rc;
   if ((g & 1) == 0 || g >= 2 * c->n) return fhe_fail(c, FHE_ERR_INVALID, "galois element must be odd and < 2N");
   if (!n_ct) return FHE_OK;
-  const size_t LN = (size_t)c->L * c->n;
-  void *ws;
-  if ((rc = ctx_workspace(c, sizeof(u64) * n_ct * 2 * LN + keyswitch_ws_bytes(c, n_ct), &ws))) return rc;
-  u64 *tmp = (u64 *)ws;
-  const bool ntt = c->params.scheme == FHE_SCHEME_CKKS;
-  if ((rc = automorph_launch(c, ct, tmp, g, 2 * n_ct, ntt))) return rc;
-  return keyswitch_ex(c, tmp + LN, 2 * c->L, gk, tmp, out, n_ct, 1u, ntt, tmp + n_ct * 2 * LN);
+  return rotate_impl(c, ct, g, gk, out, n_ct, c->params.scheme == FHE_SCHEME_CKKS);
 }
 
 int fhe_galois_elt(const fhe_ctx *c, int32_t steps, uint32_t *out) {

@@ -90,25 +90,37 @@ __global__ void __launch_bounds__(EW_BLOCK) conv_kernel(const u64 *__restrict__ 
   for (u32 m = 0; m < t.nd; ++m) d[m * N] = dot_mont<NS, SP>(v, t.h + m, t.nd, t.ns, mods[t.dst_mod[m]]);
 }
 
-// ModUp (keyswitch_one, oracle).  For digit j the digit's own limbs are
-// copied from `own` (NTT form for CKKS, coefficient form for BFV), every other
-// limb of Q u P is the fast base conversion of the digit's coefficient-form
-// limbs.  All outputs are written times R (Montgomery form) so the KS inner
-// product needs a single reduction.
+// ModUp (keyswitch_one, oracle): every limb of Q u P outside digit j is the
+// fast base conversion of the digit's coefficient-form limbs (the digit's own
+// limbs were already placed in ext by the producing kernel, ks_prep / tensor /
+// automorph).  Outputs are written times R (Montgomery form) so the KS inner
+// product needs a single reduction.  The conversion table of the digit and the
+// destination moduli are staged in LDS once per workgroup, so the per-target
+// loop issues no dependent global/scalar loads.
+#define MODUP_MAX_ND 48
 template <int NS, bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__ dc, u32 dc_stride,
-                                                         const u64 *__restrict__ own, u32 own_stride,
                                                          u64 *__restrict__ ext, const ConvTab *tabs,
                                                          const ModInfo *mods, u32 QP, u32 alpha, u32 ndig,
                                                          u32 log_n) {
+  __shared__ u64 sh_h[NS * MODUP_MAX_ND];
+  __shared__ u64 sh_q[MODUP_MAX_ND];
+  __shared__ u64 sh_aux[MODUP_MAX_ND];  // q_hi (special) or -q^-1 (generic)
+  __shared__ u32 sh_dm[MODUP_MAX_ND];
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 ct = blockIdx.y / ndig, j = blockIdx.y % ndig;
   const size_t N = (size_t)1 << log_n;
   const u32 lo = j * alpha;
   const ConvTab t = tabs[j];
-  u64 *e = ext + ((size_t)(ct * ndig + j) * QP) * N + k;
+  for (u32 x = threadIdx.x; x < t.ns * t.nd; x += EW_BLOCK) sh_h[x] = t.h[x];
+  for (u32 x = threadIdx.x; x < t.nd; x += EW_BLOCK) {
+    const u32 dm = t.dst_mod[x];
+    const ModInfo mi = mods[dm];
+    sh_dm[x] = dm;
+    sh_q[x] = mi.q;
+    sh_aux[x] = SP ? mi.q_hi : mi.qinv_neg;
+  }
   const u64 *s = dc + ((size_t)ct * dc_stride + lo) * N + k;
-  const u64 *o = own + ((size_t)ct * own_stride + lo) * N + k;
   u64 v[NS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
@@ -116,40 +128,85 @@ __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__
     if (i < (int)t.ns) {
       const ModInfo ms = mods[lo + i];
       v[i] = csub(mont_mul<SP>(s[i * N], t.hinv[i], ms), ms.q);
-      e[(lo + i) * N] = csub(mont_mul<SP>(o[i * N], ms.r2, ms), ms.q);  // own limb * R
     }
   }
-  // destinations are limbs of Q u P: dst_mod[m] is also the limb index
+  __syncthreads();
+  u64 *e = ext + ((size_t)(ct * ndig + j) * QP) * N + k;
   for (u32 m = 0; m < t.nd; ++m) {
-    const u32 dm = t.dst_mod[m];
-    e[dm * N] = dot_mont<NS, SP>(v, t.h + m, t.nd, t.ns, mods[dm]);
+    ModInfo mi;
+    mi.q = sh_q[m];
+    mi.q_hi = (u32)sh_aux[m];
+    mi.qinv_neg = sh_aux[m];
+    e[sh_dm[m] * N] = dot_mont<NS, SP>(v, sh_h + m, t.nd, t.ns, mi);
   }
+}
+
+// KS preparation for an input d (fhe_keyswitch, BFV): dc = d and the own-digit
+// slot of ext = d * R.  (mul_relin / rotate fuse this into tensor / automorph.)
+template <bool SP>
+__global__ void __launch_bounds__(EW_BLOCK) ks_prep_kernel(const u64 *__restrict__ d, u32 d_stride,
+                                                           u64 *__restrict__ dc, u64 *__restrict__ ext,
+                                                           const ModInfo *mods, u32 L, u32 QP, u32 alpha, u32 ndig,
+                                                           u32 log_n) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 ct = blockIdx.y / L, i = blockIdx.y % L, j = i / alpha;
+  const size_t N = (size_t)1 << log_n;
+  const ModInfo m = mods[i];
+  const u64 x = d[((size_t)ct * d_stride + i) * N + k];
+  dc[((size_t)ct * L + i) * N + k] = x;
+  ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub(mont_mul<SP>(x, m.r2, m), m.q);
 }
 
 // KS inner product (keyswitch_one, oracle):
 //   acc_b[i] = sum_j ext_j[i] * ksk[j][b][i]  mod m_i,  b in {0,1}
-// ext carries a factor R, removed by the one Montgomery reduction per chunk.
-template <bool SP>
+// One thread owns (limb i, coefficient k) for the WHOLE batch: the 2*dnum
+// key words are loaded once and reused by every ciphertext, so the 48 MiB key
+// is read once per call instead of once per ciphertext.  ext carries a factor
+// R, removed by the one Montgomery reduction per 4-term chunk.
+template <bool SP, int MAXD>
 __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restrict__ ext, const u64 *__restrict__ ksk,
                                                             u64 *__restrict__ acc, const ModInfo *mods, u32 QP,
-                                                            u32 ndig, u32 log_n) {
+                                                            u32 ndig, u32 n_ct, u32 log_n) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const u32 ct = blockIdx.y / QP, i = blockIdx.y % QP;
+  const u32 i = blockIdx.y;
   const size_t N = (size_t)1 << log_n;
   const ModInfo m = mods[i];
-  u64 r0 = 0, r1 = 0;
-  for (u32 j0 = 0; j0 < ndig; j0 += 4) {
-    U128 a0{0, 0}, a1{0, 0};
-    for (u32 j = j0; j < j0 + 4 && j < ndig; ++j) {
-      const u64 x = ext[((size_t)(ct * ndig + j) * QP + i) * N + k];
-      mac128(a0, x, ksk[((size_t)(2 * j) * QP + i) * N + k]);
-      mac128(a1, x, ksk[((size_t)(2 * j + 1) * QP + i) * N + k]);
+  u64 k0[MAXD], k1[MAXD];
+#pragma unroll
+  for (int j = 0; j < MAXD; ++j) {
+    if (j < (int)ndig) {
+      k0[j] = ksk[((size_t)(2 * j) * QP + i) * N + k];
+      k1[j] = ksk[((size_t)(2 * j + 1) * QP + i) * N + k];
     }
-    r0 = add_mod(r0, csub(mont_reduce<SP>(a0, m), m.q), m.q);
-    r1 = add_mod(r1, csub(mont_reduce<SP>(a1, m), m.q), m.q);
   }
-  acc[((size_t)(2 * ct) * QP + i) * N + k] = r0;
-  acc[((size_t)(2 * ct + 1) * QP + i) * N + k] = r1;
+  const size_t ext_ct = (size_t)ndig * QP * N, acc_ct = (size_t)2 * QP * N;
+  const u64 *e = ext + (size_t)i * N + k;
+  u64 *o = acc + (size_t)i * N + k;
+#pragma unroll 2
+  for (u32 ct = 0; ct < n_ct; ++ct) {
+    u64 x[MAXD];
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j)
+      if (j < (int)ndig) x[j] = e[ct * ext_ct + (size_t)j * QP * N];
+    u64 r0 = 0, r1 = 0;
+#pragma unroll
+    for (int j0 = 0; j0 < MAXD; j0 += 4) {
+      if (j0 < (int)ndig) {
+        U128 a0{0, 0}, a1{0, 0};
+#pragma unroll
+        for (int j = j0; j < j0 + 4 && j < MAXD; ++j) {
+          if (j < (int)ndig) {
+            mac128(a0, x[j], k0[j]);
+            mac128(a1, x[j], k1[j]);
+          }
+        }
+        r0 = add_mod(r0, csub(mont_reduce<SP>(a0, m), m.q), m.q);
+        r1 = add_mod(r1, csub(mont_reduce<SP>(a1, m), m.q), m.q);
+      }
+    }
+    o[ct * acc_ct] = r0;
+    o[ct * acc_ct + (size_t)QP * N] = r1;
+  }
 }
 
 // ModDown finish: out_b[i] = base_b[i] + (acc_b[i] - conv_b[i]) * P^-1 mod q_i
@@ -197,6 +254,68 @@ __global__ void __launch_bounds__(EW_BLOCK) tensor_kernel(TensorArgs t, const Mo
   mac128(s, a1, b0);
   E[t.e_poly] = reduce128<SP>(s, m);
   t.e2[ct * t.e2_ct + off] = mul_mod<SP>(a1, b1, m);
+}
+
+// CKKS ct x ct tensor fused with the key-switch preparation of d2:
+//   out[ct][0] = a0 b0, out[ct][1] = a0 b1 + a1 b0  (the relinearisation base)
+//   dc[ct] = d2 = a1 b1 (to be INTT'd in place), ext[ct][own digit] = d2 * R
+template <bool SP>
+__global__ void __launch_bounds__(EW_BLOCK) tensor_ks_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                             u64 *out, u64 *__restrict__ dc, u64 *__restrict__ ext,
+                                                             const ModInfo *mods, u32 L, u32 QP, u32 alpha,
+                                                             u32 ndig, u32 log_n) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 ct = blockIdx.y / L, i = blockIdx.y % L, j = i / alpha;
+  const size_t N = (size_t)1 << log_n, LN = (size_t)L * N;
+  const ModInfo m = mods[i];
+  const size_t o = (size_t)ct * 2 * LN + (size_t)i * N + k;
+  const u64 a0 = a[o], a1 = a[o + LN], b0 = b[o], b1 = b[o + LN];
+  out[o] = mul_mod<SP>(a0, b0, m);
+  U128 s = mul128(a0, b1);
+  mac128(s, a1, b0);
+  out[o + LN] = reduce128<SP>(s, m);
+  const u64 t = mont_reduce<SP>(mul128(a1, b1), m);  // d2 / R in [0, 2q)
+  dc[(size_t)ct * LN + (size_t)i * N + k] = csub(mont_mul<SP>(t, m.r2, m), m.q);                 // d2
+  ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub(mont_mul<SP>(mont_mul<SP>(t, m.r2, m), m.r2, m), m.q);  // d2 R
+}
+
+// Rotation input: (c0, c1) -> sigma_g, fused with the key-switch preparation:
+//   base[ct][0] = sigma(c0); dc[ct] = sigma(c1); ext[ct][own] = sigma(c1) * R.
+// NTT domain (CKKS): slot permutation; coefficient domain (BFV): signed gather.
+template <bool SP, bool NTT>
+__global__ void __launch_bounds__(EW_BLOCK) automorph_ks_kernel(const u64 *__restrict__ ct_in, u64 *__restrict__ base,
+                                                                u64 *__restrict__ dc, u64 *__restrict__ ext, u32 g,
+                                                                const ModInfo *mods, u32 L, u32 QP, u32 alpha,
+                                                                u32 ndig, u32 log_n) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 ct = blockIdx.y / L, i = blockIdx.y % L, j = i / alpha;
+  const size_t N = (size_t)1 << log_n, LN = (size_t)L * N;
+  const ModInfo m = mods[i];
+  const u64 *c0 = ct_in + (size_t)ct * 2 * LN + (size_t)i * N, *c1 = c0 + LN;
+  u64 y0, y1;
+  if (NTT) {
+    const u32 mask = (2u << log_n) - 1;
+    const u32 e = 2 * (__brev(k) >> (32 - log_n)) + 1;
+    const u32 e2 = (u32)(((u64)e * g) & mask);
+    const u32 src = __brev((e2 - 1) >> 1) >> (32 - log_n);
+    y0 = c0[src];
+    y1 = c1[src];
+  } else {
+    // here g carries g^-1 mod 2N
+    const u32 n = 1u << log_n, mask = 2 * n - 1;
+    const u32 j0 = (u32)(((u64)k * g) & mask);
+    if (j0 < n) {
+      y0 = c0[j0];
+      y1 = c1[j0];
+    } else {
+      const u64 x0 = c0[j0 - n], x1 = c1[j0 - n];
+      y0 = x0 ? m.q - x0 : 0;
+      y1 = x1 ? m.q - x1 : 0;
+    }
+  }
+  base[(size_t)ct * 2 * LN + (size_t)i * N + k] = y0;
+  dc[(size_t)ct * LN + (size_t)i * N + k] = y1;
+  ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub(mont_mul<SP>(y1, m.r2, m), m.q);
 }
 
 // NTT-domain automorphism (orc_automorph_ntt): slot k holds a(psi^(2brv(k)+1))
@@ -357,24 +476,60 @@ int conv_impl(fhe_ctx *c, const ConvTab &t, const u64 *src, u32 ss, u64 *dst, u3
 }
 
 template <bool SP>
-int modup_impl(fhe_ctx *c, const u64 *dc, u32 dcs, const u64 *own, u32 owns, u64 *ext, u32 n, u32 ndig) {
+int modup_impl(fhe_ctx *c, const u64 *dc, u32 dcs, u64 *ext, u32 n, u32 ndig) {
   dim3 grid(c->n / EW_BLOCK, n * ndig);
   const u32 QP = c->L + c->K;
   if (c->alpha <= 4)
-    hipLaunchKernelGGL((modup_kernel<4, SP>), grid, dim3(EW_BLOCK), 0, c->stream, dc, dcs, own, owns, ext, c->d_modup, c->d_mods, QP, c->alpha, ndig, c->log_n);
+    hipLaunchKernelGGL((modup_kernel<4, SP>), grid, dim3(EW_BLOCK), 0, c->stream, dc, dcs, ext, c->d_modup, c->d_mods, QP, c->alpha, ndig, c->log_n);
   else if (c->alpha <= 8)
-    hipLaunchKernelGGL((modup_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, dc, dcs, own, owns, ext, c->d_modup, c->d_mods, QP, c->alpha, ndig, c->log_n);
+    hipLaunchKernelGGL((modup_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, dc, dcs, ext, c->d_modup, c->d_mods, QP, c->alpha, ndig, c->log_n);
   else
-    hipLaunchKernelGGL((modup_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, dc, dcs, own, owns, ext, c->d_modup, c->d_mods, QP, c->alpha, ndig, c->log_n);
+    hipLaunchKernelGGL((modup_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, dc, dcs, ext, c->d_modup, c->d_mods, QP, c->alpha, ndig, c->log_n);
   return fhe_check(c, hipGetLastError(), "modup_kernel");
 }
 
 template <bool SP>
 int inner_impl(fhe_ctx *c, const u64 *ext, const u64 *ksk, u64 *acc, u32 n, u32 ndig) {
   const u32 QP = c->L + c->K;
-  hipLaunchKernelGGL((ks_inner_kernel<SP>), dim3(c->n / EW_BLOCK, n * QP), dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc,
-                     c->d_mods, QP, ndig, c->log_n);
+  dim3 grid(c->n / EW_BLOCK, QP);
+  if (ndig <= 4)
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 4>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
+  else if (ndig <= 8)
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 8>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
+  else
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 48>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
   return fhe_check(c, hipGetLastError(), "ks_inner_kernel");
+}
+
+template <bool SP>
+int ks_prep_impl(fhe_ctx *c, const u64 *d, u32 d_stride, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+  hipLaunchKernelGGL((ks_prep_kernel<SP>), dim3(c->n / EW_BLOCK, n * c->L), dim3(EW_BLOCK), 0, c->stream, d, d_stride,
+                     dc, ext, c->d_mods, c->L, c->L + c->K, c->alpha, ndig, c->log_n);
+  return fhe_check(c, hipGetLastError(), "ks_prep_kernel");
+}
+
+template <bool SP>
+int tensor_ks_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+  hipLaunchKernelGGL((tensor_ks_kernel<SP>), dim3(c->n / EW_BLOCK, n * c->L), dim3(EW_BLOCK), 0, c->stream, a, b, out,
+                     dc, ext, c->d_mods, c->L, c->L + c->K, c->alpha, ndig, c->log_n);
+  return fhe_check(c, hipGetLastError(), "tensor_ks_kernel");
+}
+
+template <bool SP>
+int automorph_ks_impl(fhe_ctx *c, const u64 *ct, u64 *base, u64 *dc, u64 *ext, u32 g, u32 n, u32 ndig, bool ntt) {
+  dim3 grid(c->n / EW_BLOCK, n * c->L);
+  const u32 QP = c->L + c->K;
+  if (ntt) {
+    hipLaunchKernelGGL((automorph_ks_kernel<SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, ct, base, dc, ext, g,
+                       c->d_mods, c->L, QP, c->alpha, ndig, c->log_n);
+  } else {
+    u32 inv = g;  // g^-1 mod 2N (g odd) by Newton iteration on the 2-adic inverse
+    for (int i = 0; i < 5; ++i) inv *= 2u - g * inv;
+    inv &= (2u * c->n) - 1;
+    hipLaunchKernelGGL((automorph_ks_kernel<SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, ct, base, dc, ext, inv,
+                       c->d_mods, c->L, QP, c->alpha, ndig, c->log_n);
+  }
+  return fhe_check(c, hipGetLastError(), "automorph_ks_kernel");
 }
 
 template <bool SP>
@@ -442,30 +597,40 @@ size_t keyswitch_ws_bytes(const fhe_ctx *c, u32 n) {
   return sizeof(u64) * N * n * (L + c->dnum * QP + 2 * QP + 2 * L);
 }
 
-// Hybrid key switching, batched over n inputs (keyswitch_one, oracle).
-//   d   : [n][d_stride limbs], the L limbs of item i at d + i*d_stride*N
-//         (NTT form iff ntt_form, i.e. CKKS)
+// Key-switch scratch layout (keyswitch_ws_bytes):
+//   dc   [n][L][N]        the input d; INTT'd in place for CKKS
+//   ext  [n][ndig][QP][N] ModUp output times R (own-digit limbs written by the producer)
+//   acc  [n][2][QP][N]    inner product
+//   conv [n][2][L][N]     ModDown conversion
+struct KsWs {
+  u64 *dc, *ext, *acc, *conv;
+  u32 ndig;
+};
+static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
+  const size_t L = c->L, QP = c->L + c->K, N = c->n;
+  KsWs w;
+  w.ndig = (c->L + c->alpha - 1) / c->alpha;
+  w.dc = ws;
+  w.ext = w.dc + n * L * N;
+  w.acc = w.ext + n * w.ndig * QP * N;
+  w.conv = w.acc + n * 2 * QP * N;
+  return w;
+}
+
+// Hybrid key switching on a PREPARED scratch (dc and the own-digit limbs of
+// ext filled by ks_prep / tensor_ks / automorph_ks).
 //   out : [n][2][L][N], out_b = (add_mask bit b ? base_b : 0) + KS(d)_b;
-//         base may alias out (element-wise), d must not alias out.
-int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u64 *base, u64 *out, u32 n,
-                 u32 add_mask, bool ntt_form, u64 *ws) {
-  const u32 L = c->L, K = c->K, QP = L + K, N = c->n;
-  const u32 ndig = (L + c->alpha - 1) / c->alpha;
-  u64 *dc = ws;                                   // [n][L][N]
-  u64 *ext = dc + (size_t)n * L * N;              // [n][ndig][QP][N]
-  u64 *acc = ext + (size_t)n * ndig * QP * N;     // [n][2][QP][N]
-  u64 *conv = acc + (size_t)n * 2 * QP * N;       // [n][2][L][N]
+//         base may alias out (element-wise).
+static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
+                         bool ntt_form) {
+  const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
+  u64 *dc = w.dc, *ext = w.ext, *acc = w.acc, *conv = w.conv;
   int rc;
-  // 1. coefficient-form copy of d
-  rc = fhe_check(c, hipMemcpy2DAsync(dc, (size_t)L * N * 8, d, (size_t)d_stride * N * 8, (size_t)L * N * 8, n,
-                                     hipMemcpyDeviceToDevice, c->stream), "ks copy");
-  if (rc) return rc;
   if (ntt_form) {
     if ((rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true))) return rc;
   }
-  // 2. ModUp all digits.  Own limbs: NTT-form d for CKKS; coefficient-form dc for BFV (NTT'd below)
-  if ((rc = SP_DISPATCH(c, modup_impl, c, dc, L, ntt_form ? d : dc, ntt_form ? d_stride : L, ext, n, ndig)))
-    return rc;
+  // 2. ModUp: every non-own limb of every digit
+  if ((rc = SP_DISPATCH(c, modup_impl, c, dc, L, ext, n, ndig))) return rc;
   // 3. NTT the converted limbs (all limbs for BFV, whose own limbs are coefficient form)
   for (u32 j = 0; j < ndig; ++j) {
     const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
@@ -483,6 +648,38 @@ int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u
   }
   // 6. combine
   return SP_DISPATCH(c, combine_impl, c, acc, conv, base, out, n, add_mask);
+}
+
+// Hybrid key switching of an arbitrary input d ([n][d_stride limbs], the L
+// limbs first; NTT form iff ntt_form).  d must not alias out.
+int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u64 *base, u64 *out, u32 n,
+                 u32 add_mask, bool ntt_form, u64 *ws) {
+  const KsWs w = ks_layout(c, n, ws);
+  int rc = SP_DISPATCH(c, ks_prep_impl, c, d, d_stride, w.dc, w.ext, n, w.ndig);
+  if (rc) return rc;
+  return keyswitch_run(c, w, ksk, base, out, n, add_mask, ntt_form);
+}
+
+// CKKS ct x ct: tensor (fused with the KS preparation of d2) + relinearise.
+int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n) {
+  void *ws;
+  int rc = ctx_workspace(c, keyswitch_ws_bytes(c, n), &ws);
+  if (rc) return rc;
+  const KsWs w = ks_layout(c, n, (u64 *)ws);
+  if ((rc = SP_DISPATCH(c, tensor_ks_impl, c, a, b, out, w.dc, w.ext, n, w.ndig))) return rc;
+  return keyswitch_run(c, w, rlk, out, out, n, 3u, true);
+}
+
+// Rotation: automorphism (fused with the KS preparation of sigma(c1)) + KS.
+int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n, bool ntt_form) {
+  const size_t LN = (size_t)c->L * c->n;
+  void *ws;
+  int rc = ctx_workspace(c, sizeof(u64) * n * 2 * LN + keyswitch_ws_bytes(c, n), &ws);
+  if (rc) return rc;
+  u64 *base = (u64 *)ws;  // [n][2][L][N], poly 0 = sigma(c0)
+  const KsWs w = ks_layout(c, n, base + n * 2 * LN);
+  if ((rc = SP_DISPATCH(c, automorph_ks_impl, c, ct, base, w.dc, w.ext, g, n, w.ndig, ntt_form))) return rc;
+  return keyswitch_run(c, w, gk, base, out, n, 1u, ntt_form);
 }
 
 int tensor_launch(fhe_ctx *c, const u64 *a, size_t a_ct, size_t a_poly, const u64 *b, size_t b_ct, size_t b_poly,
