@@ -96,42 +96,49 @@ HD u64 mont_reduce(U128 T, const ModInfo &m) {
 // q = q_hi * 2^32 + 1.  Six v_mad_u64_u32 and no 128-bit carry chains: the
 // bounds a_hi < 2^31 and b_hi < 2^29 keep every partial sum below 2^64.
 // Returns a*b*2^-64 mod q in [0, 1.5q).
+// Each "+ (p0 != 0)" carry of a Montgomery round is folded into the multiply-add
+// that produces the word: P' = a0 b0 + (2^32 - 1) has P'.hi = P.hi + (P.lo != 0)
+// and ~P'.lo = -P.lo mod 2^32.  OPAQUE keeps the compiler from rewriting
+// ~P'.lo back into a (slow) v_mul_lo_u32 of the operands.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define OPAQUE(x) asm("" : "+v"(x))
+#else
+#define OPAQUE(x) (void)0
+#endif
 HD u64 mont_mul_sp(u64 a, u64 b, u32 q_hi) {
   const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
-  const u64 P = (u64)a0 * b0;
-  const u64 U = (u64)a1 * b0 + (P >> 32);            // t = U : P_lo
-  const u32 p0 = (u32)P;
-  const u64 V = (u64)(0u - p0) * q_hi + U + (p0 != 0);  // (t + m q) / 2^32
-  const u64 X0 = (u64)a0 * b1 + V;                   // t' = V + a b1 = X1 : x0
-  const u32 x0 = (u32)X0;
-  const u64 X1 = (u64)a1 * b1 + (X0 >> 32);
-  return (u64)(0u - x0) * q_hi + X1 + (x0 != 0);
+  u64 P = (u64)a0 * b0 + 0xFFFFFFFFull;
+  OPAQUE(P);
+  u64 V = (u64)(~(u32)P) * q_hi + ((u64)a1 * b0 + (P >> 32));  // (a b0 + m q) / 2^32
+  OPAQUE(V);
+  u64 X0 = (u64)a0 * b1 + V + 0xFFFFFFFFull;                         // + a0 b1, carry folded
+  OPAQUE(X0);
+  return (u64)(~(u32)X0) * q_hi + ((u64)a1 * b1 + (X0 >> 32));
 }
 
 // M independent mont_mul_sp products written phase by phase, so the
-// quarter-rate multiply chains of different products interleave in the
-// instruction stream instead of each serial chain stalling the wave.
+// multiply chains of different products interleave in the instruction stream.
 template <int M>
 HD void mont_mul_sp_vec(u64 (&r)[M], const u64 (&a)[M], const u64 (&b)[M], u32 q_hi) {
   u64 t[M];
 #pragma unroll
-  for (int i = 0; i < M; ++i) t[i] = (u64)(u32)a[i] * (u32)b[i];                      // P
-#pragma unroll
-  for (int i = 0; i < M; ++i) r[i] = (u64)(u32)(a[i] >> 32) * (u32)b[i] + (t[i] >> 32);  // U
-#pragma unroll
   for (int i = 0; i < M; ++i) {
-    const u32 p0 = (u32)t[i];
-    t[i] = (u64)(0u - p0) * q_hi + r[i] + (p0 != 0);                                   // V
+    t[i] = (u64)(u32)a[i] * (u32)b[i] + 0xFFFFFFFFull;  // P'
+    OPAQUE(t[i]);
   }
 #pragma unroll
-  for (int i = 0; i < M; ++i) t[i] = (u64)(u32)a[i] * (u32)(b[i] >> 32) + t[i];        // X0
-#pragma unroll
-  for (int i = 0; i < M; ++i) r[i] = (u64)(u32)(a[i] >> 32) * (u32)(b[i] >> 32) + (t[i] >> 32);  // X1
+  for (int i = 0; i < M; ++i) {
+    t[i] = (u64)(~(u32)t[i]) * q_hi + ((u64)(u32)(a[i] >> 32) * (u32)b[i] + (t[i] >> 32));  // V
+    OPAQUE(t[i]);  // keep the mad chain as written (no re-association into extra adds)
+  }
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    const u32 x0 = (u32)t[i];
-    r[i] = (u64)(0u - x0) * q_hi + r[i] + (x0 != 0);
+    t[i] = (u64)(u32)a[i] * (u32)(b[i] >> 32) + t[i] + 0xFFFFFFFFull;  // X0'
+    OPAQUE(t[i]);
   }
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+    r[i] = (u64)(~(u32)t[i]) * q_hi + ((u64)(u32)(a[i] >> 32) * (u32)(b[i] >> 32) + (t[i] >> 32));
 }
 
 template <bool SP>

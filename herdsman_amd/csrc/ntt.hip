@@ -98,16 +98,23 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
           ++n;
         }
       }
+      // 64-bit adds of SGPR constants as single v_lshl_add_u64 (no carry
+      // chain through VCC, which costs s_nop wait states): a - b = a + (2q+1) + ~b - 2q
+      u64 nq2 = 0 - q2, q2p1 = q2 + 1;
+      asm("" : "+s"(nq2));
+      asm("" : "+s"(q2p1));
 #pragma unroll
       for (int i = 0; i < H; ++i) {
         const u64 X = x[lo_idx[i]], Y = x[lo_idx[i] + half];
         if (!INV) {
-          U[i] = X >= q2 ? X - q2 : X;
+          const u64 d = X + nq2;
+          U[i] = (int64_t)d < 0 ? X : d;
           A[i] = Y;
         } else {
           const u64 sm = X + Y;
-          U[i] = sm >= q2 ? sm - q2 : sm;
-          A[i] = X - Y + q2;
+          const u64 d = sm + nq2;
+          U[i] = (int64_t)d < 0 ? sm : d;
+          A[i] = (X + q2p1) + ~Y;
         }
       }
       mont_mul_sp_vec<H>(V, A, Wt, mi.q_hi);
@@ -115,7 +122,7 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
       for (int i = 0; i < H; ++i) {
         if (!INV) {
           x[lo_idx[i]] = U[i] + V[i];
-          x[lo_idx[i] + half] = U[i] - V[i] + q2;
+          x[lo_idx[i] + half] = (U[i] + q2p1) + ~V[i];
         } else {
           x[lo_idx[i]] = U[i];
           x[lo_idx[i] + half] = V[i];
