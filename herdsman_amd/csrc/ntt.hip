@@ -22,6 +22,8 @@
 // passes, 16 contiguous words per lane for row passes), and each group's
 // twiddles are fetched while the previous group computes, so neither the
 // data nor the twiddle latency sits on the VALU critical path.
+#include <algorithm>
+
 #include "context.hpp"
 
 namespace {
@@ -35,6 +37,25 @@ struct NttArgs {
   u32 s0;                // first global stage of this pass
   u32 log_stride;        // sub-transform element stride = 2^log_stride
   u32 last;              // canonicalise output (and scale by N^-1 for INTT)
+  // EPI_COMBINE (forward last pass over the ModDown conversion conv [p][L][N],
+  // p = 2 ct + b): out[p][i] = (add_mask bit b ? base[p][i] : 0) + (acc[p][i] - conv) P^-1
+  const u64 *e_acc;      // [p][e_acc_stride][N]
+  const u64 *e_base;     // [p][L][N], may alias e_out
+  u64 *e_out;            // [p][L][N]
+  const u64 *e_pinv;     // [L] P^-1 R mod q_i
+  u32 e_acc_stride;
+  u32 e_add_mask;
+};
+
+enum { EPI_NONE = 0, EPI_COMBINE = 1 };
+
+// per-workgroup epilogue operands (resolved once per limb)
+struct EpiRow {
+  const u64 *acc;
+  const u64 *base;
+  u64 *out;
+  u64 pinv;
+  bool add;
 };
 
 template <int S>
@@ -152,10 +173,10 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
   }
 }
 
-template <int S, int LOGR, int W, bool INV, bool COLS, bool SP, int GI>
+template <int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int GI>
 __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds, const u64 *tw, u64 *data,
                                            size_t gb, u32 stride, u32 w, u32 ts, u32 hi, const NttArgs &a,
-                                           const ModInfo &mi, u32 mod) {
+                                           const ModInfo &mi, u32 mod, const EpiRow &ep) {
   constexpr int NG = (S + LOGR - 1) / LOGR;
   constexpr int R = 1 << LOGR;
   constexpr int G = INV ? NG - 1 - GI : GI;
@@ -171,7 +192,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = lds[lds_idx<S>(w, Grp<S, LOGR, GN>::k_of(r, ts))];
-    group_loop<S, LOGR, W, INV, COLS, SP, GI + 1>(x, tn, lds, tw, data, gb, stride, w, ts, hi, a, mi, mod);
+    group_loop<S, LOGR, W, INV, COLS, SP, EPI, GI + 1>(x, tn, lds, tw, data, gb, stride, w, ts, hi, a, mi, mod, ep);
   } else {
     run_group<S, LOGR, G, INV, SP>(x, tc, q2, mi);
     if (a.last) {
@@ -191,17 +212,31 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
       for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, GP::k_of(r, ts))] = x[r];
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        data[gb + Grp<S, LOGR, 0>::k_of(r, ts)] = lds[lds_idx<S>(w, Grp<S, LOGR, 0>::k_of(r, ts))];
+      for (int r = 0; r < R; ++r) {
+        const u32 k = Grp<S, LOGR, 0>::k_of(r, ts);
+        const u64 v = lds[lds_idx<S>(w, k)];
+        if constexpr (EPI == EPI_COMBINE) {
+          // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM
+          const size_t o = gb + k;
+          u64 ks = csub(mont_mul<SP>(sub_mod(ep.acc[o], v, q), ep.pinv, mi), q);
+          if (ep.add) ks = add_mod(ks, ep.base[o], q);
+          ep.out[o] = ks;
+        } else {
+          data[gb + k] = v;
+        }
+      }
     } else {
+      static_assert(EPI == EPI_NONE, "epilogues run in the re-laid-out row store");
 #pragma unroll
       for (int r = 0; r < R; ++r) data[gb + (size_t)GP::k_of(r, ts) * stride] = x[r];
     }
   }
 }
 
-template <int S, int LOGR, int W, bool INV, bool COLS, bool SP>
+template <int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI>
 __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
+  static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE, "ntt_pass epilogues");
+  static_assert(EPI == EPI_NONE || (!INV && !COLS), "epilogues follow a forward row pass");
   constexpr int R = 1 << LOGR;
   constexpr int T = 1 << (S - LOGR);
   constexpr int NG = (S + LOGR - 1) / LOGR;
@@ -245,10 +280,18 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = data[gb + (size_t)Grp<S, LOGR, G0>::k_of(r, ts) * stride];
   }
-  group_loop<S, LOGR, W, INV, COLS, SP, 0>(x, tc, lds, tw, data, gb, stride, w, ts, hi, a, mi, mod);
+  EpiRow ep{};
+  if constexpr (EPI == EPI_COMBINE) {
+    ep.acc = a.e_acc + (((size_t)poly * a.e_acc_stride + limb) << a.log_n);
+    ep.base = a.e_base + (((size_t)poly * a.map.poly_stride + limb) << a.log_n);
+    ep.out = a.e_out + (((size_t)poly * a.map.poly_stride + limb) << a.log_n);
+    ep.pinv = a.e_pinv[limb];
+    ep.add = (a.e_add_mask >> (poly & 1)) & 1;
+  }
+  group_loop<S, LOGR, W, INV, COLS, SP, EPI, 0>(x, tc, lds, tw, data, gb, stride, w, ts, hi, a, mi, mod, ep);
 }
 
-template <int S, int W, bool COLS, bool INV, bool SP>
+template <int S, int W, bool COLS, bool INV, bool SP, int EPI>
 int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   constexpr int LOGR = 4;
   constexpr int NT = W << (S - LOGR);
@@ -256,30 +299,39 @@ int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   constexpr size_t lds = (size_t)W * (SUB + (SUB >> 4) + 1) * sizeof(u64);
   const u32 subs = 1u << (a.log_n - S);
   dim3 grid(subs / W, n_jobs);
-  auto k = ntt_pass<S, LOGR, W, INV, COLS, SP>;
+  auto k = ntt_pass<S, LOGR, W, INV, COLS, SP, EPI>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);
   return fhe_check(c, hipGetLastError(), "ntt_pass launch");
 }
 
-template <int S, int W, bool COLS>
+template <int S, int W, bool COLS, int EPI = EPI_NONE>
 int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
-  if (c->special)
-    return inv ? launch_one<S, W, COLS, true, true>(c, a, n_jobs) : launch_one<S, W, COLS, false, true>(c, a, n_jobs);
-  return inv ? launch_one<S, W, COLS, true, false>(c, a, n_jobs) : launch_one<S, W, COLS, false, false>(c, a, n_jobs);
+  if constexpr (EPI != EPI_NONE) {
+    if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
+    return c->special ? launch_one<S, W, COLS, false, true, EPI>(c, a, n_jobs)
+                      : launch_one<S, W, COLS, false, false, EPI>(c, a, n_jobs);
+  } else {
+    if (c->special)
+      return inv ? launch_one<S, W, COLS, true, true, EPI>(c, a, n_jobs)
+                 : launch_one<S, W, COLS, false, true, EPI>(c, a, n_jobs);
+    return inv ? launch_one<S, W, COLS, true, false, EPI>(c, a, n_jobs)
+               : launch_one<S, W, COLS, false, false, EPI>(c, a, n_jobs);
+  }
 }
 
 // one pass over a whole residue (N <= 2^14)
+template <int EPI = EPI_NONE>
 int single_pass(fhe_ctx *c, NttArgs a, bool inv, u32 n_jobs) {
   a.s0 = 0;
   a.log_stride = 0;
   a.last = 1;
   switch (a.log_n) {
-    case 10: return launch_pass<10, 1, false>(c, a, inv, n_jobs);
-    case 11: return launch_pass<11, 1, false>(c, a, inv, n_jobs);
-    case 12: return launch_pass<12, 1, false>(c, a, inv, n_jobs);
-    case 13: return launch_pass<13, 1, false>(c, a, inv, n_jobs);
-    case 14: return launch_pass<14, 1, false>(c, a, inv, n_jobs);
+    case 10: return launch_pass<10, 1, false, EPI>(c, a, inv, n_jobs);
+    case 11: return launch_pass<11, 1, false, EPI>(c, a, inv, n_jobs);
+    case 12: return launch_pass<12, 1, false, EPI>(c, a, inv, n_jobs);
+    case 13: return launch_pass<13, 1, false, EPI>(c, a, inv, n_jobs);
+    case 14: return launch_pass<14, 1, false, EPI>(c, a, inv, n_jobs);
   }
   return fhe_fail(c, FHE_ERR_UNSUPPORTED, "single_pass: log_n");
 }
@@ -297,13 +349,14 @@ int col_pass(fhe_ctx *c, NttArgs a, bool inv, u32 n_jobs, bool last) {
 }
 
 // row pass: stages [S1, logN), contiguous blocks
+template <int EPI = EPI_NONE>
 int row_pass(fhe_ctx *c, NttArgs a, bool inv, u32 n_jobs, bool last) {
   a.log_stride = 0;
   a.last = last;
   switch (a.log_n) {
-    case 15: a.s0 = 7; return launch_pass<8, 16, false>(c, a, inv, n_jobs);
-    case 16: a.s0 = 8; return launch_pass<8, 16, false>(c, a, inv, n_jobs);
-    case 17: a.s0 = 8; return launch_pass<9, 8, false>(c, a, inv, n_jobs);
+    case 15: a.s0 = 7; return launch_pass<8, 16, false, EPI>(c, a, inv, n_jobs);
+    case 16: a.s0 = 8; return launch_pass<8, 16, false, EPI>(c, a, inv, n_jobs);
+    case 17: a.s0 = 8; return launch_pass<9, 8, false, EPI>(c, a, inv, n_jobs);
   }
   return fhe_fail(c, FHE_ERR_UNSUPPORTED, "row_pass: log_n");
 }
@@ -341,4 +394,40 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse) {
   rc = row_pass(c, a, true, n_jobs, false);
   if (rc) return rc;
   return col_pass(c, a, true, n_jobs, true);
+}
+
+// Forward NTT of the ModDown conversion conv (all L limbs of 2n polys) with
+// the ModDown finish fused into its last pass (EPI_COMBINE):
+//   out[p][i] = (add_mask bit (p & 1) ? base[p][i] : 0) + (acc[p][i] - NTT(conv)[p][i]) P^-1  mod q_i
+// conv is transformed in place by the first pass only; acc rows have stride acc_stride limbs.
+int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
+                           u64 *out, u32 add_mask) {
+  const u32 L = c->L;
+  const size_t N = c->n;
+  const u32 per = 65535u / L;  // gridDim.y
+  for (u32 p0 = 0; p0 < n_polys; p0 += per) {
+    const u32 np = std::min(per, n_polys - p0);
+    NttArgs a{};
+    a.map = LimbMap{conv + (size_t)p0 * L * N, L, L, 0, L, 0, 0, np};
+    a.tw = c->d_tw_fwd;
+    a.mods = c->d_mods;
+    a.ninv = c->d_ninv;
+    a.log_n = c->log_n;
+    a.e_acc = acc + (size_t)p0 * acc_stride * N;
+    a.e_base = base + (size_t)p0 * L * N;
+    a.e_out = out + (size_t)p0 * L * N;
+    a.e_pinv = c->d_pinv;
+    a.e_acc_stride = acc_stride;
+    a.e_add_mask = add_mask;
+    const u32 n_jobs = np * L;
+    int rc;
+    if (c->log_n <= 14) {
+      rc = single_pass<EPI_COMBINE>(c, a, false, n_jobs);
+    } else {
+      if ((rc = col_pass(c, a, false, n_jobs, false))) return rc;
+      rc = row_pass<EPI_COMBINE>(c, a, false, n_jobs, true);
+    }
+    if (rc) return rc;
+  }
+  return FHE_OK;
 }

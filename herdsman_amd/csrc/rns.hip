@@ -643,10 +643,8 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   // 5. ModDown: INTT the P part (all of Q u P for BFV), convert P -> Q
   if ((rc = ntt_launch(c, LimbMap{acc, QP, ntt_form ? K : QP, ntt_form ? L : 0, QP, 0, 0, 2 * n}, true))) return rc;
   if ((rc = conv_launch(c, c->moddown, acc + (size_t)L * N, QP, conv, L, 2 * n))) return rc;
-  if (ntt_form) {
-    if ((rc = ntt_launch(c, LimbMap{conv, L, L, 0, L, 0, 0, 2 * n}, false))) return rc;
-  }
-  // 6. combine
+  // 6. combine: fused into the last pass of NTT(conv) for NTT-form results
+  if (ntt_form) return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask);
   return SP_DISPATCH(c, combine_impl, c, acc, conv, base, out, n, add_mask);
 }
 

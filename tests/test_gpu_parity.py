@@ -135,9 +135,12 @@ def test_ckks_golden(hb):
     assert np.array_equal(hb.to_host(out)[0], g["out_conj"])
 
 
-@pytest.mark.parametrize("log_n,L,K,dnum,n_ct", [(12, 5, 2, 3, 3), (16, 12, 4, 3, 2)])
+@pytest.mark.parametrize("log_n,L,K,dnum,n_ct", [(12, 5, 2, 3, 3), (16, 12, 4, 3, 2), (15, 5, 2, 2, 3),
+                                                (17, 3, 2, 3, 1)])
 def test_ckks_mul_relin_vs_oracle(hb, log_n, L, K, dnum, n_ct):
-    """(16, 12, 4, 3) is the BASELINE metric config (ct-mult+relin, N=2^16, L=12)."""
+    """(16, 12, 4, 3) is the BASELINE metric config (ct-mult+relin, N=2^16, L=12).
+    log_n 15..17 run the two-pass NTT whose last pass carries the fused ModDown finish
+    (ragged digits at 15)."""
     o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum)
     a = o.uniform((n_ct, 2, L, 1 << log_n), seed=10)
     b = o.uniform((n_ct, 2, L, 1 << log_n), seed=11)
@@ -164,9 +167,12 @@ def test_ckks_rotate_c4(hb):
         assert np.array_equal(hb.to_host(dout), want), steps
 
 
-def test_keyswitch_vs_oracle(hb):
-    o, c = pair(hb, SCHEME_CKKS, 13, 7, 3, 3)  # ragged digits: alpha=3, last digit has 1 limb
-    d = o.uniform((2, 7, 1 << 13), seed=30)
+@pytest.mark.parametrize("log_n,L,K,dnum", [(13, 7, 3, 3), (15, 8, 2, 4), (15, 5, 1, 5)])
+def test_keyswitch_vs_oracle(hb, log_n, L, K, dnum):
+    """(13,7,3,3): ragged digits (alpha=3, last digit 1 limb); (15,8,2,4): 4 digits;
+    (15,5,1,5): 5 single-limb digits."""
+    o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum)
+    d = o.uniform((2, L, 1 << log_n), seed=30)
     k = o.uniform(o.key_shape(), seed=31)
     want = o.keyswitch(d, k)
     dout = hb.empty(want.shape)
