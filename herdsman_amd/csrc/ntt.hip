@@ -58,12 +58,21 @@ struct EpiRow {
   bool add;
 };
 
+// LDS slot of element k of sub-transform w: one pad word per 16 words and per
+// sub-transform keeps every exchange pattern free of bank conflicts
+// (SQ_LDS_BANK_CONFLICT = 0), and the slot stays affine in the register index
+// r, so the 16 accesses of a thread share one address register.
 template <int S>
 __device__ __forceinline__ u32 lds_idx(u32 w, u32 k) {
   constexpr u32 SUB = 1u << S;
   constexpr u32 PAD = SUB + (SUB >> 4) + 1;
   return w * PAD + k + (k >> 4);
 }
+template <int S, int W>
+constexpr size_t lds_bytes() {
+  return (size_t)W * ((1u << S) + (1u << S >> 4) + 1) * sizeof(u64);
+}
+
 
 // Group geometry (compile time): group g covers local stages
 // [g*LOGR, g*LOGR + nb); its butterfly bits are k bits [p, p+nb).  A thread
@@ -295,8 +304,7 @@ template <int S, int W, bool COLS, bool INV, bool SP, int EPI>
 int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   constexpr int LOGR = 4;
   constexpr int NT = W << (S - LOGR);
-  constexpr size_t SUB = 1u << S;
-  constexpr size_t lds = (size_t)W * (SUB + (SUB >> 4) + 1) * sizeof(u64);
+  constexpr size_t lds = lds_bytes<S, W>();
   const u32 subs = 1u << (a.log_n - S);
   dim3 grid(subs / W, n_jobs);
   auto k = ntt_pass<S, LOGR, W, INV, COLS, SP, EPI>;

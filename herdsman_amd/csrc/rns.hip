@@ -21,6 +21,13 @@
 
 namespace {
 
+// Streaming stores/loads for data that is written or read exactly once per
+// kernel and consumed by a later kernel (far larger than L2/MALL).
+template <typename T>
+__device__ __forceinline__ void st_nt(T *p, T v) { __builtin_nontemporal_store(v, p); }
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T *p) { return __builtin_nontemporal_load(p); }
+
 // sum_{i < ns} v[i] * h[i * hs] mod m, exact, given canonical v[i] and
 // R-pre-scaled constants h.  Chunks of 4 keep each 128-bit sum < q * 2^64.
 template <int NS, bool SP>
@@ -87,7 +94,7 @@ __global__ void __launch_bounds__(EW_BLOCK) conv_kernel(const u64 *__restrict__ 
       v[i] = csub(mont_mul<SP>(s[i * N], t.hinv[i], ms), ms.q);
     }
   }
-  for (u32 m = 0; m < t.nd; ++m) d[m * N] = dot_mont<NS, SP>(v, t.h + m, t.nd, t.ns, mods[t.dst_mod[m]]);
+  for (u32 m = 0; m < t.nd; ++m) st_nt(d + m * N, dot_mont<NS, SP>(v, t.h + m, t.nd, t.ns, mods[t.dst_mod[m]]));
 }
 
 // ModUp (keyswitch_one, oracle): every limb of Q u P outside digit j is the
@@ -127,7 +134,7 @@ __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__
     v[i] = 0;
     if (i < (int)t.ns) {
       const ModInfo ms = mods[lo + i];
-      v[i] = csub(mont_mul<SP>(s[i * N], t.hinv[i], ms), ms.q);
+      v[i] = csub(mont_mul<SP>(ld_nt(s + i * N), t.hinv[i], ms), ms.q);
     }
   }
   __syncthreads();
@@ -137,7 +144,7 @@ __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__
     mi.q = sh_q[m];
     mi.q_hi = (u32)sh_aux[m];
     mi.qinv_neg = sh_aux[m];
-    e[sh_dm[m] * N] = dot_mont<NS, SP>(v, sh_h + m, t.nd, t.ns, mi);
+    st_nt(e + sh_dm[m] * N, dot_mont<NS, SP>(v, sh_h + m, t.nd, t.ns, mi));
   }
 }
 
@@ -187,7 +194,7 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restric
     u64 x[MAXD];
 #pragma unroll
     for (int j = 0; j < MAXD; ++j)
-      if (j < (int)ndig) x[j] = e[ct * ext_ct + (size_t)j * QP * N];
+      if (j < (int)ndig) x[j] = ld_nt(e + ct * ext_ct + (size_t)j * QP * N);
     u64 r0 = 0, r1 = 0;
 #pragma unroll
     for (int j0 = 0; j0 < MAXD; j0 += 4) {
@@ -204,8 +211,8 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restric
         r1 = add_mod(r1, csub(mont_reduce<SP>(a1, m), m.q), m.q);
       }
     }
-    o[ct * acc_ct] = r0;
-    o[ct * acc_ct + (size_t)QP * N] = r1;
+    st_nt(o + ct * acc_ct, r0);
+    st_nt(o + ct * acc_ct + (size_t)QP * N, r1);
   }
 }
 
@@ -269,14 +276,15 @@ __global__ void __launch_bounds__(EW_BLOCK) tensor_ks_kernel(const u64 *__restri
   const size_t N = (size_t)1 << log_n, LN = (size_t)L * N;
   const ModInfo m = mods[i];
   const size_t o = (size_t)ct * 2 * LN + (size_t)i * N + k;
-  const u64 a0 = a[o], a1 = a[o + LN], b0 = b[o], b1 = b[o + LN];
-  out[o] = mul_mod<SP>(a0, b0, m);
+  const u64 a0 = ld_nt(a + o), a1 = ld_nt(a + o + LN), b0 = ld_nt(b + o), b1 = ld_nt(b + o + LN);
+  st_nt(out + o, mul_mod<SP>(a0, b0, m));
   U128 s = mul128(a0, b1);
   mac128(s, a1, b0);
-  out[o + LN] = reduce128<SP>(s, m);
+  st_nt(out + o + LN, reduce128<SP>(s, m));
   const u64 t = mont_reduce<SP>(mul128(a1, b1), m);  // d2 / R in [0, 2q)
-  dc[(size_t)ct * LN + (size_t)i * N + k] = csub(mont_mul<SP>(t, m.r2, m), m.q);                 // d2
-  ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub(mont_mul<SP>(mont_mul<SP>(t, m.r2, m), m.r2, m), m.q);  // d2 R
+  st_nt(dc + (size_t)ct * LN + (size_t)i * N + k, csub(mont_mul<SP>(t, m.r2, m), m.q));                 // d2
+  st_nt(ext + ((size_t)(ct * ndig + j) * QP + i) * N + k,
+        csub(mont_mul<SP>(mont_mul<SP>(t, m.r2, m), m.r2, m), m.q));  // d2 R
 }
 
 // Rotation input: (c0, c1) -> sigma_g, fused with the key-switch preparation:
