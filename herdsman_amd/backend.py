@@ -68,8 +68,14 @@ SIGNATURES = {
     "fhe_keyswitch": (C.c_int, [_vp, _vp, _vp, _vp, _u32]),
     "fhe_rotate": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _u32]),
     "fhe_galois_elt": (C.c_int, [_vp, _i32, C.POINTER(_u32)]),
+    "fhe_reduce": (C.c_int, [_vp, _vp, _u32, C.c_int, _vp, _vp]),
     "fhe_bcast_key": (C.c_int, [_vp, _vp, _sz, _vp, C.c_int]),
+    "fhe_reduce_ranks": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, C.c_int, _vp]),
+    "fhe_reduce_schedule": (C.c_int, [C.c_int, C.c_int, C.c_int, _vp, C.c_int]),
 }
+
+REDUCE_ADD = 0
+REDUCE_MUL_RELIN = 1
 
 _lib = None
 
@@ -226,6 +232,13 @@ class Context:
         self._ck(self.lib.fhe_rotate(self.h, _ptr(ct), galois, _ptr(gk), _ptr(out), ct.shape[0]), "fhe_rotate")
         return out
 
+    def reduce(self, cts, op: int, rlk=None, out=None):
+        """Balanced-tree reduction of cts [n][2][L][N] to out [1][2][L][N] (cts is scratch)."""
+        out = cts[:1] if out is None else out
+        self._ck(self.lib.fhe_reduce(self.h, _ptr(cts), cts.shape[0], op, _ptr(rlk) if rlk is not None else None,
+                                     _ptr(out)), "fhe_reduce")
+        return out
+
     def galois_elt(self, steps: int) -> int:
         g = _u32()
         self._ck(self.lib.fhe_galois_elt(self.h, steps, C.byref(g)), "fhe_galois_elt")
@@ -251,3 +264,14 @@ def empty(shape, device="cuda"):
     import torch
 
     return torch.empty(shape, dtype=torch.int64, device=device)
+
+
+def reduce_schedule(rank: int, world: int, root: int = 0):
+    """fhe_reduce_schedule: this rank's steps of the cross-rank tree, as
+    ("recv", peer) / ("send", peer) pairs (host only, no device needed)."""
+    lib = load_library()
+    buf = (C.c_int32 * 32)()
+    n = lib.fhe_reduce_schedule(rank, world, root, C.cast(buf, _vp), 32)
+    if n < 0:
+        raise FheBackendError(f"fhe_reduce_schedule({rank}, {world}, {root}) = {n}")
+    return [("recv", v - 1) if v > 0 else ("send", -v - 1) for v in buf[:n]]

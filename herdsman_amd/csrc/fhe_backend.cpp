@@ -469,6 +469,72 @@ int fhe_galois_elt(const fhe_ctx *c, int32_t steps, uint32_t *out) {
   return FHE_OK;
 }
 
+static int combine(fhe_ctx *c, int op, uint64_t *a, const uint64_t *b, const uint64_t *rlk, uint32_t n) {
+  return op == FHE_REDUCE_ADD ? fhe_add(c, a, b, a, n) : fhe_mul_relin(c, a, b, rlk, a, n);
+}
+
+int fhe_reduce(fhe_ctx *c, uint64_t *cts, uint32_t n_ct, int op, const uint64_t *rlk, uint64_t *out) {
+  if (!c) return FHE_ERR_INVALID;
+  if (!cts || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
+  if (op != FHE_REDUCE_ADD && op != FHE_REDUCE_MUL_RELIN) return fhe_fail(c, FHE_ERR_INVALID, "reduce op");
+  if (op == FHE_REDUCE_MUL_RELIN && !rlk) return fhe_fail(c, FHE_ERR_INVALID, "reduce MUL_RELIN needs rlk");
+  if (n_ct == 0) return fhe_fail(c, FHE_ERR_INVALID, "reduce over no ciphertexts");
+  const size_t cw = (size_t)2 * c->L * c->n;
+  for (uint32_t live = n_ct; live > 1;) {
+    const uint32_t half = live / 2;
+    int rc = combine(c, op, cts, cts + (size_t)(live - half) * cw, rlk, half);
+    if (rc) return rc;
+    live -= half;
+  }
+  if (out != cts) return fhe_check(c, hipMemcpyAsync(out, cts, cw * 8, hipMemcpyDeviceToDevice, c->stream), "copy");
+  return FHE_OK;
+}
+
+int fhe_reduce_schedule(int rank, int world, int root, int32_t *steps, int cap) {
+  if (world < 1 || rank < 0 || rank >= world || root < 0 || root >= world || (!steps && cap > 0)) return FHE_ERR_INVALID;
+  const int rel = (rank - root + world) % world;
+  int n = 0;
+  for (int s = 1; s < world; s <<= 1) {
+    if (rel % (2 * s) == s) {  // send the partial result one level up, then stop
+      if (n >= cap) return FHE_ERR_INVALID;
+      steps[n++] = -(((rel - s + root) % world) + 1);
+      break;
+    }
+    if (rel % (2 * s) == 0 && rel + s < world) {
+      if (n >= cap) return FHE_ERR_INVALID;
+      steps[n++] = ((rel + s + root) % world) + 1;
+    }
+  }
+  return n;
+}
+
+int fhe_reduce_ranks(fhe_ctx *c, uint64_t *ct, int op, const uint64_t *rlk, void *comm, int root, uint64_t *tmp) {
+  if (!c) return FHE_ERR_INVALID;
+  if (!ct || !comm || !tmp) return fhe_fail(c, FHE_ERR_INVALID, "null argument");
+  if (op != FHE_REDUCE_ADD && op != FHE_REDUCE_MUL_RELIN) return fhe_fail(c, FHE_ERR_INVALID, "reduce op");
+  if (op == FHE_REDUCE_MUL_RELIN && !rlk) return fhe_fail(c, FHE_ERR_INVALID, "reduce MUL_RELIN needs rlk");
+  int rank = 0, world = 1;
+  if (ncclCommUserRank((ncclComm_t)comm, &rank) != ncclSuccess || ncclCommCount((ncclComm_t)comm, &world) != ncclSuccess)
+    return fhe_fail(c, FHE_ERR_DEVICE, "RCCL communicator query");
+  int32_t steps[32];
+  const int n = fhe_reduce_schedule(rank, world, root, steps, 32);
+  if (n < 0) return fhe_fail(c, FHE_ERR_INVALID, "reduce schedule (root / world)");
+  const size_t cw = (size_t)2 * c->L * c->n;
+  for (int i = 0; i < n; ++i) {
+    ncclResult_t r;
+    if (steps[i] > 0) {
+      r = ncclRecv(tmp, cw, ncclUint64, steps[i] - 1, (ncclComm_t)comm, c->stream);
+      if (r != ncclSuccess) return fhe_fail(c, FHE_ERR_DEVICE, std::string("ncclRecv: ") + ncclGetErrorString(r));
+      const int rc = combine(c, op, ct, tmp, rlk, 1);
+      if (rc) return rc;
+    } else {
+      r = ncclSend(ct, cw, ncclUint64, -steps[i] - 1, (ncclComm_t)comm, c->stream);
+      if (r != ncclSuccess) return fhe_fail(c, FHE_ERR_DEVICE, std::string("ncclSend: ") + ncclGetErrorString(r));
+    }
+  }
+  return FHE_OK;
+}
+
 int fhe_bcast_key(fhe_ctx *c, uint64_t *key, size_t words, void *comm, int root) {
   if (!c || !key || !comm) return fhe_fail(c, FHE_ERR_INVALID, "null argument");
   ncclResult_t r = ncclBroadcast(key, key, words, ncclUint64, root, (ncclComm_t)comm, c->stream);

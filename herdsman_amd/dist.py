@@ -10,7 +10,7 @@ floor(rows/P) rows, +1 for p < rows mod P, storage_service.cpp:121-129).
 from __future__ import annotations
 
 import os
-from typing import Tuple
+from typing import Callable, List, Tuple
 
 
 def world() -> Tuple[int, int, int]:
@@ -45,3 +45,39 @@ def max_over_ranks(x: float, device=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def reduce_schedule(rank: int, world_size: int, root: int = 0) -> List[Tuple[str, int]]:
+    """Binomial tree towards `root` (the schedule of fhe_reduce_ranks): at level
+    s = 1, 2, 4, ... a rank whose offset from root is an odd multiple of s sends
+    its partial result to offset - s and stops; one at an even multiple receives
+    from offset + s (when that rank exists) and combines."""
+    if world_size < 1 or not (0 <= rank < world_size and 0 <= root < world_size):
+        raise ValueError("bad rank / world / root")
+    rel, steps, s = (rank - root) % world_size, [], 1
+    while s < world_size:
+        if rel % (2 * s) == s:
+            steps.append(("send", (rel - s + root) % world_size))
+            break
+        if rel % (2 * s) == 0 and rel + s < world_size:
+            steps.append(("recv", (rel + s + root) % world_size))
+        s *= 2
+    return steps
+
+
+def reduce_ranks(ct, combine: Callable, scratch, root: int = 0) -> None:
+    """Join per-rank partial results with torch.distributed
+    point-to-point transfers (RCCL on GPU tensors, gloo on CPU ones):
+    combine(ct, scratch) folds a received ciphertext into ct, e.g. a batched
+    mod-q add (ctx.add) or mul+relin on the GPU.  The result is in ct on root.
+    The C ABI's fhe_reduce_ranks runs the same tree with ncclSend/ncclRecv."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    rank, world_size = dist.get_rank(), dist.get_world_size()
+    for kind, peer in reduce_schedule(rank, world_size, root):
+        if kind == "recv":
+            dist.recv(scratch, src=peer)
+            combine(ct, scratch)
+        else:
+            dist.send(ct, dst=peer)

@@ -392,16 +392,9 @@ void GpuWorkerGroup::device_loop(Device &dev) {
         if (count == 0) throw std::runtime_error("reduce over no rows");
         DevBuf a(s.ctx, count * cw);
         ck(s.ctx, fhe_memcpy_h2d(s.ctx, a.p, host.data(), count * cw * 8), "h2d");
-        // level by level: the first `half` items absorb the last `half`; an odd
-        // middle item stays in place, so the survivors are always a prefix
-        size_t live = count;
-        while (live > 1) {
-          const size_t half = live / 2;
-          uint64_t *lo = a.p, *hi = a.p + (live - half) * cw;
-          if (mul) ck(s.ctx, fhe_mul_relin(s.ctx, lo, hi, ks->relin.p, lo, (uint32_t)half), "reduce mul");
-          else ck(s.ctx, fhe_add(s.ctx, lo, hi, lo, (uint32_t)half), "reduce add");
-          live -= half;
-        }
+        // balanced tree, one batched add / mul+relin per level (fhe_reduce)
+        ck(s.ctx, fhe_reduce(s.ctx, a.p, (uint32_t)count, mul ? FHE_REDUCE_MUL_RELIN : FHE_REDUCE_ADD,
+                             mul ? ks->relin.p : nullptr, a.p), "reduce");
         std::vector<uint64_t> res(cw);
         ck(s.ctx, fhe_memcpy_d2h(s.ctx, res.data(), a.p, cw * 8), "d2h");
         write_partition(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr), {make_row(s, res.data())});

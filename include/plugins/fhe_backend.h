@@ -115,11 +115,34 @@ int fhe_rotate(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const uint
 /* 5^steps mod 2N (steps may be negative); conjugation is 2N-1 */
 int fhe_galois_elt(const fhe_ctx *ctx, int32_t steps, uint32_t *out);
 
+/* ---- reductions ---------------------------------------
+ * Homomorphic reduction of n_ct ciphertexts to one, the evaluation of one
+ * herdsman ReduceTask (the cross-partition tree itself is planned by
+ * /root/reference/src/service/execution_service.cpp:590-688).  Balanced tree,
+ * one batched fhe_add / fhe_mul_relin per level: at a level with `live`
+ * survivors, item i < live/2 absorbs item i + live - live/2 (an odd middle
+ * item waits a level).  cts is the scratch and is overwritten; the result is
+ * written to out (which may alias cts).  op MUL_RELIN needs rlk. */
+#define FHE_REDUCE_ADD 0
+#define FHE_REDUCE_MUL_RELIN 1
+int fhe_reduce(fhe_ctx *ctx, uint64_t *cts, uint32_t n_ct, int op, const uint64_t *rlk, uint64_t *out);
+
 /* ---- multi-GPU ---------------------------------------------------------
  * Broadcast an evaluation key (words u64 in device memory) from `root` to all
  * ranks of an RCCL communicator (ncclComm_t passed as void*).  The only
  * collective the backend uses. */
 int fhe_bcast_key(fhe_ctx *ctx, uint64_t *key, size_t words, void *nccl_comm, int root);
+/* Join of per-rank partial results: every rank holds one ciphertext `ct`
+ * ([2][L][N]); a binomial tree of RCCL point-to-point transfers
+ * (ncclSend/ncclRecv over xGMI) moves them towards `root`, and the receiving
+ * rank combines with the mod-q op of `op` (RCCL has no modular reduction).
+ * The result is in `ct` on root; tmp is one ciphertext of device scratch. */
+int fhe_reduce_ranks(fhe_ctx *ctx, uint64_t *ct, int op, const uint64_t *rlk, void *nccl_comm, int root,
+                     uint64_t *tmp);
+/* The tree of fhe_reduce_ranks, host only: writes the rank's steps in order,
+ * peer + 1 for "receive from peer and combine", -(peer + 1) for "send to peer
+ * (then stop)"; returns the number of steps (<= cap) or a negative error. */
+int fhe_reduce_schedule(int rank, int world, int root, int32_t *steps, int cap);
 
 #ifdef __cplusplus
 }

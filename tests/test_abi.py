@@ -32,7 +32,7 @@ def lib():
 def test_header_declares_the_operator_surface():
     names = declared_functions()
     for op in ("fhe_ntt_fwd", "fhe_ntt_inv", "fhe_add", "fhe_mul_relin", "fhe_keyswitch", "fhe_rotate",
-               "fhe_bcast_key", "fhe_base_conv"):
+               "fhe_bcast_key", "fhe_base_conv", "fhe_reduce", "fhe_reduce_ranks"):
         assert op in names
 
 
@@ -67,3 +67,16 @@ def test_no_gpu_means_loud_failure(lib):
     import herdsman_amd.backend as hb
     with pytest.raises(hb.FheBackendError):
         hb.Context(hb.SCHEME_CKKS, 12, 2)
+
+
+def test_reduce_schedule_c_matches_python(lib):
+    """fhe_reduce_schedule (host-only ABI function; the tree fhe_reduce_ranks runs
+    with RCCL) equals herdsman_amd.dist.reduce_schedule (the gloo-tested tree)."""
+    import herdsman_amd.backend as hb
+    from herdsman_amd.dist import reduce_schedule
+    for world in range(1, 17):
+        for root in range(world):
+            for rank in range(world):
+                assert hb.reduce_schedule(rank, world, root) == reduce_schedule(rank, world, root)
+    with pytest.raises(hb.FheBackendError):
+        hb.reduce_schedule(2, 2, 0)

@@ -201,6 +201,37 @@ def test_ckks_real_keys_decrypt(hb):
     assert max(abs(x - y) for x, y in zip(dec, want)) < 2 ** 56
 
 
+def _tree_expected(o, cts, combine):
+    """fhe_reduce's pairing: item i < live/2 absorbs item i + live - live/2."""
+    cts = cts.copy()
+    live = cts.shape[0]
+    while live > 1:
+        half = live // 2
+        cts[:half] = combine(cts[:half], cts[live - half:live])
+        live -= half
+    return cts[:1]
+
+
+def test_reduce_tree_ckks(hb):
+    """fhe_reduce (ReduceTask evaluation): add and mul+relin trees
+    over an odd count, bit-exact against the oracle's ops in the same pairing."""
+    o, c = pair(hb, SCHEME_CKKS, 12, 3, 2, 2)
+    cts = o.uniform((5, 2, 3, 1 << 12), seed=80)
+    rlk = o.uniform(o.key_shape(), seed=81)
+    want_add = _tree_expected(o, cts, o.ct_add)
+    want_mul = _tree_expected(o, cts, lambda a, b: o.mul_relin(a, b, rlk))
+    d = hb.to_device(cts)
+    out = hb.empty((1, 2, 3, 1 << 12))
+    c.reduce(d, hb.REDUCE_ADD, out=out)
+    assert np.array_equal(hb.to_host(out), want_add)
+    d = hb.to_device(cts)
+    c.reduce(d, hb.REDUCE_MUL_RELIN, hb.to_device(rlk), out=out)
+    assert np.array_equal(hb.to_host(out), want_mul)
+    one = hb.to_device(cts[:1])
+    c.reduce(one, hb.REDUCE_ADD, out=out)
+    assert np.array_equal(hb.to_host(out), cts[:1])
+
+
 # --------------------------------------------------------------------- BFV
 def test_bfv_golden(hb):
     g = load("bfv_n1024_l4.npz")

@@ -66,3 +66,79 @@ def test_gloo_world2_key_broadcast_and_timing():
     assert all(r[1] for r in res), "key broadcast mismatch"
     assert all(r[2] == 1.0 for r in res), "max over ranks"
     assert res[0][3:] == (0, 4096) and res[1][3:] == (4096, 8192)
+
+
+# ---------------------------------------------------------------- reduce tree
+Q_TEST = 2147483647  # small modulus: the int64 stand-in combine below cannot overflow
+K_MIX = 1000003
+
+
+def _mix(a, b):
+    """Non-commutative stand-in for a ciphertext combine (a <- a*K + b mod q): the
+    result pins WHICH partial results were combined in WHICH order."""
+    a.mul_(K_MIX).add_(b).remainder_(Q_TEST)
+
+
+def _simulate(world, root, init):
+    """Expected root value, level by level: at level s the rank at offset rel
+    (rel % 2s == 0) absorbs the one at rel + s, which finished its own levels."""
+    vals = {rel: init((rel + root) % world) for rel in range(world)}
+    s = 1
+    while s < world:
+        for rel in range(0, world, 2 * s):
+            if rel + s < world:
+                vals[rel] = (vals[rel] * K_MIX + vals[rel + s]) % Q_TEST
+        s *= 2
+    return vals[0]
+
+
+def _init(rank):
+    return (rank + 1) * 7919 + 13
+
+
+def _reduce_worker(rank, world, root, port, q):
+    import torch.distributed as dist
+    from herdsman_amd.dist import reduce_ranks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ct = torch.full((2, 3, 16), _init(rank), dtype=torch.int64)
+        scratch = torch.empty_like(ct)
+        reduce_ranks(ct, _mix, scratch, root=root)
+        q.put((rank, int(ct[0, 0, 0]), bool((ct == ct[0, 0, 0]).all())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,root", [(2, 0), (3, 0), (4, 1)])
+def test_gloo_reduce_ranks_tree(world, root):
+    """The cross-rank join of per-rank partial results delivers
+    exactly the binomial-tree combination to root."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reduce_worker, args=(r, world, root, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (v, uni)) for r, v, uni in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[root][1]
+    assert res[root][0] == _simulate(world, root, _init)
+
+
+def test_reduce_schedule_is_a_tree():
+    """Every non-root rank sends exactly once, to a rank that receives from it."""
+    from herdsman_amd.dist import reduce_schedule
+    for world in range(1, 17):
+        for root in range(world):
+            sched = {r: reduce_schedule(r, world, root) for r in range(world)}
+            sends = {r: [p for k, p in s if k == "send"] for r, s in sched.items()}
+            assert sends[root] == []
+            for r in range(world):
+                if r == root:
+                    continue
+                assert len(sends[r]) == 1 and sched[r][-1][0] == "send"
+                assert ("recv", r) in sched[sends[r][0]]
+            assert sum(len(s) for s in sched.values()) == 2 * (world - 1)
