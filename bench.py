@@ -127,11 +127,12 @@ def main():
     ntt_ms = e0.elapsed_time(e1) / reps
     algo_bytes = limbs * 2 * n * 8
     achieved = algo_bytes / (ntt_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = valu_busy = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             traffic = tj.get("hbm_bytes_per_limb_ntt")
+            valu_busy = tj.get("valu_busy")
             if traffic is not None:
                 traffic = traffic * limbs
         except Exception:
@@ -173,6 +174,9 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes": algo_bytes,
                 "launch_ms": round(ntt_ms, 4),
+                # the NTT is integer-VALU bound, not HBM bound: share of the
+                # SIMDs' issue slots running VALU work (PMC, profiles/)
+                "valu_busy": valu_busy,
             },
             "ntt_fwd_limb_per_s": round(ntt_limb_per_s, 1),
             "key_bcast_ms": round(key_bcast_ms, 3),

@@ -16,4 +16,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fe
   python3 bench.py --roofline-only --no-cpu > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
   python3 bench.py --roofline-only --no-cpu > "$OUT/pmc_write.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES GRBM_GUI_ACTIVE --output-format csv \
+  -d "$OUT/pmc_valu" -o run -- python3 bench.py --roofline-only --no-cpu > "$OUT/pmc_valu.log" 2>&1
 echo profile done
