@@ -164,6 +164,25 @@ HD u64 reduce128(U128 T, const ModInfo &m) {
   return csub(mont_mul<SP>(mont_reduce<SP>(T, m), m.r2, m), m.q);
 }
 
+// sum_{i < ns} v[i] * h[i * hs] mod m, exact, given canonical v[i] and
+// R-pre-scaled constants h.  Chunks of 4 keep each 128-bit sum < q * 2^64.
+template <int NS, bool SP>
+HD u64 dot_mont(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
+  u64 res = 0;
+#pragma unroll
+  for (int c0 = 0; c0 < NS; c0 += 4) {
+    if (c0 < (int)ns) {
+      U128 acc{0, 0};
+#pragma unroll
+      for (int i = c0; i < c0 + 4 && i < NS; ++i)
+        if (i < (int)ns) mac128(acc, v[i], h[(size_t)i * hs]);
+      const u64 part = csub(mont_reduce<SP>(acc, m), m.q);
+      res = c0 == 0 ? part : add_mod(res, part, m.q);
+    }
+  }
+  return res;
+}
+
 // SplitMix64 stream shared with the oracle (orc_fill_uniform)
 HD u64 splitmix64(u64 z) {
   z ^= z >> 30;

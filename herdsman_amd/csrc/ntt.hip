@@ -62,6 +62,14 @@ struct EpiRow {
 // sub-transform keeps every exchange pattern free of bank conflicts
 // (SQ_LDS_BANK_CONFLICT = 0), and the slot stays affine in the register index
 // r, so the 16 accesses of a thread share one address register.
+// Element access at a 32-bit word index from a scalar (per-workgroup) base:
+// the byte offset is formed in 32 bits so the load/store uses the
+// `global_load v, v_off, s[base:base+1]` form (one VALU op per address).
+__device__ __forceinline__ u64 ld_at(const u64 *base, u32 idx) {
+  return *(const u64 *)((const char *)base + (idx << 3));
+}
+__device__ __forceinline__ void st_at(u64 *base, u32 idx, u64 v) { *(u64 *)((char *)base + (idx << 3)) = v; }
+
 template <int S>
 __device__ __forceinline__ u32 lds_idx(u32 w, u32 k) {
   constexpr u32 SUB = 1u << S;
@@ -99,10 +107,19 @@ struct Grp {
         for (int d = 0; d < (1 << tau); ++d) {
           const u32 sigma = G * LOGR + tau;
           const u32 kk = ((((hh << ex) | rx) << tau) | d);
-          t[slot(tau, rx, d)] = tw[(1u << (s0 + sigma)) + (hi << sigma) + kk];
+          t[slot(tau, rx, d)] = ld_at(tw, (1u << (s0 + sigma)) + (hi << sigma) + kk);
         }
   }
 };
+
+// x - m if that is non-negative, else x (x, m < 2^63; neg_m = -m), selected
+// by the sign word with two v_bfi_b32: no VCC compare/select, so no hazard nops
+__device__ __forceinline__ u64 harvey_csub(u64 x, u64 neg_m) {
+  const u64 d = x + neg_m;
+  const u32 m = (u32)((int32_t)(u32)(d >> 32) >> 31);  // all ones iff d < 0
+  const u64 mm = ((u64)m << 32) | m;
+  return (x & mm) | (d & ~mm);
+}
 
 template <int S, int LOGR, int G, bool INV, bool SP>
 __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 q2, const ModInfo &mi) {
@@ -137,13 +154,10 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
       for (int i = 0; i < H; ++i) {
         const u64 X = x[lo_idx[i]], Y = x[lo_idx[i] + half];
         if (!INV) {
-          const u64 d = X + nq2;
-          U[i] = (int64_t)d < 0 ? X : d;
+          U[i] = harvey_csub(X, nq2);
           A[i] = Y;
         } else {
-          const u64 sm = X + Y;
-          const u64 d = sm + nq2;
-          U[i] = (int64_t)d < 0 ? sm : d;
+          U[i] = harvey_csub(X + Y, nq2);
           A[i] = (X + q2p1) + ~Y;
         }
       }
@@ -184,7 +198,7 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
 
 template <int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int GI>
 __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds, const u64 *tw, u64 *data,
-                                           size_t gb, u32 stride, u32 w, u32 ts, u32 hi, const NttArgs &a,
+                                           u32 gb, u32 stride, u32 w, u32 ts, u32 hi, const NttArgs &a,
                                            const ModInfo &mi, u32 mod, const EpiRow &ep) {
   constexpr int NG = (S + LOGR - 1) / LOGR;
   constexpr int R = 1 << LOGR;
@@ -207,11 +221,11 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     if (a.last) {
       if (!INV) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = csub(csub(x[r], q2), q);
+        for (int r = 0; r < R; ++r) x[r] = harvey_csub(harvey_csub(x[r], 0 - q2), 0 - q);
       } else {
         const u64 sc = a.ninv[mod];
 #pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = csub(mont_mul<SP>(x[r], sc, mi), q);
+        for (int r = 0; r < R; ++r) x[r] = harvey_csub(mont_mul<SP>(x[r], sc, mi), 0 - q);
       }
     }
     if constexpr (!COLS && G != 0) {
@@ -226,18 +240,18 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
         const u64 v = lds[lds_idx<S>(w, k)];
         if constexpr (EPI == EPI_COMBINE) {
           // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM
-          const size_t o = gb + k;
-          u64 ks = csub(mont_mul<SP>(sub_mod(ep.acc[o], v, q), ep.pinv, mi), q);
-          if (ep.add) ks = add_mod(ks, ep.base[o], q);
-          ep.out[o] = ks;
+          const u32 o = gb + k;
+          u64 ks = harvey_csub(mont_mul<SP>(sub_mod(ld_at(ep.acc, o), v, q), ep.pinv, mi), 0 - q);
+          if (ep.add) ks = add_mod(ks, ld_at(ep.base, o), q);
+          st_at(ep.out, o, ks);
         } else {
-          data[gb + k] = v;
+          st_at(data, gb + k, v);
         }
       }
     } else {
       static_assert(EPI == EPI_NONE, "epilogues run in the re-laid-out row store");
 #pragma unroll
-      for (int r = 0; r < R; ++r) data[gb + (size_t)GP::k_of(r, ts) * stride] = x[r];
+      for (int r = 0; r < R; ++r) st_at(data, gb + (GP::k_of(r, ts) << a.log_stride), x[r]);
     }
   }
 }
@@ -252,10 +266,11 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   static_assert(R == 16, "register tile is 16 words");
   extern __shared__ u64 lds[];
 
+  // (poly, limb) come from gridDim.y / gridDim.z, so every per-workgroup
+  // quantity is scalar (SGPR) and element addresses are 32-bit offsets from a
+  // scalar base (global_load ... saddr): no 64-bit VALU address arithmetic
   const u32 tid = threadIdx.x;
-  const u32 e = blockIdx.y;
-  const u32 cnt = a.map.cnt;
-  const u32 poly = e / cnt, act = e - poly * cnt;
+  const u32 poly = blockIdx.y, act = blockIdx.z;
   const u32 limb = limbmap_limb(a.map, act);
   const u32 mod = a.map.mod_offset + limb;
   u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << a.log_n);
@@ -269,7 +284,7 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   if (COLS) { w = tid % W; ts = tid / W; } else { ts = tid % T; w = tid / T; }
   const u32 u = blockIdx.x * W + w;
   const u32 hi = u >> a.log_stride;
-  const size_t gb = ((size_t)hi << (S + a.log_stride)) + (u & (stride - 1));
+  const u32 gb = (hi << (S + a.log_stride)) + (u & (stride - 1));
 
   constexpr int G0 = INV ? NG - 1 : 0;
   u64 tc[16];
@@ -279,7 +294,7 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
     // row pass starting in a per-lane-contiguous group: coalesced load in the
     // group-0 layout, then one LDS re-layout
 #pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = data[gb + Grp<S, LOGR, 0>::k_of(r, ts)];
+    for (int r = 0; r < R; ++r) x[r] = ld_at(data, gb + Grp<S, LOGR, 0>::k_of(r, ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, Grp<S, LOGR, 0>::k_of(r, ts))] = x[r];
     __syncthreads();
@@ -287,7 +302,7 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
     for (int r = 0; r < R; ++r) x[r] = lds[lds_idx<S>(w, Grp<S, LOGR, G0>::k_of(r, ts))];
   } else {
 #pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = data[gb + (size_t)Grp<S, LOGR, G0>::k_of(r, ts) * stride];
+    for (int r = 0; r < R; ++r) x[r] = ld_at(data, gb + (Grp<S, LOGR, G0>::k_of(r, ts) << a.log_stride));
   }
   EpiRow ep{};
   if constexpr (EPI == EPI_COMBINE) {
@@ -306,7 +321,9 @@ int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   constexpr int NT = W << (S - LOGR);
   constexpr size_t lds = lds_bytes<S, W>();
   const u32 subs = 1u << (a.log_n - S);
-  dim3 grid(subs / W, n_jobs);
+  // dispatch order: row blocks, then polys, then limbs -- the resident
+  // workgroups share one modulus, so its twiddle table stays in L2
+  dim3 grid(subs / W, n_jobs / a.map.cnt, a.map.cnt);
   auto k = ntt_pass<S, LOGR, W, INV, COLS, SP, EPI>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);
@@ -374,9 +391,9 @@ int row_pass(fhe_ctx *c, NttArgs a, bool inv, u32 n_jobs, bool last) {
 int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse) {
   const u32 n_jobs = m.n_polys * m.cnt;
   if (n_jobs == 0) return FHE_OK;
-  if (n_jobs > 65535u) {
+  if (m.n_polys > 65535u) {
     // split along polys to respect gridDim.y
-    u32 per = 65535u / m.cnt;
+    const u32 per = 65535u;
     for (u32 p0 = 0; p0 < m.n_polys; p0 += per) {
       LimbMap sub = m;
       sub.base = m.base + (size_t)p0 * m.poly_stride * c->n;
@@ -412,7 +429,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
                            u64 *out, u32 add_mask) {
   const u32 L = c->L;
   const size_t N = c->n;
-  const u32 per = 65535u / L;  // gridDim.y
+  const u32 per = 65535u;  // gridDim.y
   for (u32 p0 = 0; p0 < n_polys; p0 += per) {
     const u32 np = std::min(per, n_polys - p0);
     NttArgs a{};

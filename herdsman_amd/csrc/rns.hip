@@ -28,25 +28,6 @@ __device__ __forceinline__ void st_nt(T *p, T v) { __builtin_nontemporal_store(v
 template <typename T>
 __device__ __forceinline__ T ld_nt(const T *p) { return __builtin_nontemporal_load(p); }
 
-// sum_{i < ns} v[i] * h[i * hs] mod m, exact, given canonical v[i] and
-// R-pre-scaled constants h.  Chunks of 4 keep each 128-bit sum < q * 2^64.
-template <int NS, bool SP>
-__device__ __forceinline__ u64 dot_mont(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
-  u64 res = 0;
-#pragma unroll
-  for (int c0 = 0; c0 < NS; c0 += 4) {
-    if (c0 < (int)ns) {
-      U128 acc{0, 0};
-#pragma unroll
-      for (int i = c0; i < c0 + 4 && i < NS; ++i)
-        if (i < (int)ns) mac128(acc, v[i], h[(size_t)i * hs]);
-      const u64 part = csub(mont_reduce<SP>(acc, m), m.q);
-      res = c0 == 0 ? part : add_mod(res, part, m.q);
-    }
-  }
-  return res;
-}
-
 // ------------------------------------------------------------ element-wise
 template <EwOp OP, bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) ew_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
@@ -634,9 +615,8 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
   u64 *dc = w.dc, *ext = w.ext, *acc = w.acc, *conv = w.conv;
   int rc;
-  if (ntt_form) {
-    if ((rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true))) return rc;
-  }
+  // 1. INTT d (CKKS)
+  if (ntt_form && (rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true))) return rc;
   // 2. ModUp: every non-own limb of every digit
   if ((rc = SP_DISPATCH(c, modup_impl, c, dc, L, ext, n, ndig))) return rc;
   // 3. NTT the converted limbs (all limbs for BFV, whose own limbs are coefficient form)
