@@ -18,6 +18,8 @@ Extra fields:
                   bytes = 2 * N * 8 per limb-NTT (read + write the residue once).
   cpu_baseline -- the CPU oracle (oracle/fhe_oracle.c, OpenMP over ciphertexts)
                   on a bounded sample of the same workload, rank 0 at N=1 only.
+  secondary    -- per-GPU throughput of the other BASELINE configs: C4 rotate,
+                  C3 BFV mul+relin, C2 NTT (not part of `value`).
 """
 from __future__ import annotations
 
@@ -46,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline duration")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary measurements (C4 rotate, C3 BFV mul+relin, C2 NTT)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the timed NTT loop (for rocprofv3 runs of the dominant kernel)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "ntt_traffic.json"))
@@ -139,6 +143,10 @@ def main():
             traffic = None
     ntt_limb_per_s = limbs / (ntt_ms * 1e-3)
 
+    secondary = None
+    if not (args.roofline_only or args.no_secondary):
+        secondary = secondary_configs(hb, ctx, rlk, a, out, dev, stream, B, max(2, args.steps // 2))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, ctx)
@@ -182,10 +190,53 @@ def main():
             "key_bcast_ms": round(key_bcast_ms, 3),
             "algorithmic_GBps_ct_mult": round(value / world * 6 * L * n * 8 / 1e9, 1),
             "cpu_baseline": cpu,
+            "secondary": secondary,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _timed(fn, reps, stream):
+    import torch
+    fn()  # warm (workspace, caches)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3
+
+
+def secondary_configs(hb, ctx, gk, ct, out, dev, stream, B, reps):
+    """Per-GPU throughput of the other BASELINE.json configs (same synthetic-data rules):
+    C4 CKKS rotate + hybrid KS at the metric parameters (B ciphertexts per call),
+    C3 BFV mul+relin at N=2^15 L=8 (BEHZ), C2 forward+inverse NTT at N=2^14 L=4."""
+    res = {}
+    g = ctx.galois_elt(1)
+    t = _timed(lambda: ctx.rotate(ct, g, gk, out), reps, stream)
+    res["C4_ckks_rotate_per_s"] = round(B / t, 1)
+    bfv = hb.Context(hb.SCHEME_BFV, 15, 8, 4, 2, t=65537, device=dev.index)
+    bfv.set_stream(stream)
+    n3 = 1 << 15
+    a3 = bfv.fill_uniform(hb.empty((B, 2, 8, n3), device=dev), seed=31)
+    b3 = bfv.fill_uniform(hb.empty((B, 2, 8, n3), device=dev), seed=32)
+    k3 = bfv.fill_uniform(hb.empty(bfv.key_shape(), device=dev), seed=33)
+    o3 = hb.empty((B, 2, 8, n3), device=dev)
+    t = _timed(lambda: bfv.mul_relin(a3, b3, k3, o3), reps, stream)
+    res["C3_bfv_mul_relin_per_s"] = round(B / t, 1)
+    del a3, b3, k3, o3
+    bfv.close()
+    c2 = hb.Context(hb.SCHEME_CKKS, 14, 4, device=dev.index)
+    c2.set_stream(stream)
+    polys = 256
+    x2 = c2.fill_uniform(hb.empty((polys, 4, 1 << 14), device=dev), seed=21)
+    t = _timed(lambda: (c2.ntt_fwd(x2), c2.ntt_inv(x2)), reps, stream)
+    res["C2_ntt_fwd_inv_poly_per_s"] = round(polys / t, 1)
+    res["C2_limb_ntt_per_s"] = round(2 * 4 * polys / t, 1)
+    c2.close()
+    return res
 
 
 def cpu_baseline(args, ctx):

@@ -352,28 +352,30 @@ int fhe_memcpy_d2h(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
   return fhe_check(c, hipStreamSynchronize(c->stream), "d2h sync");
 }
 
-static int check_range(fhe_ctx *c, const void *p, uint32_t mod_begin, uint32_t n_limbs) {
+// an empty batch (count == 0) is a no-op that accepts null buffers
+static int check_range(fhe_ctx *c, const void *p, uint32_t mod_begin, uint32_t n_limbs, uint32_t count) {
   if (!c) return FHE_ERR_INVALID;
-  if (!p) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   if (n_limbs == 0 || mod_begin + n_limbs > c->nmod) return fhe_fail(c, FHE_ERR_INVALID, "modulus range");
+  if (!p && count) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   return FHE_OK;
 }
 
 int fhe_ntt_fwd(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs) {
-  int rc = check_range(c, data, mod_begin, n_limbs);
+  int rc = check_range(c, data, mod_begin, n_limbs, n_polys);
   if (rc) return rc;
   return ntt_launch(c, LimbMap{data, n_limbs, n_limbs, 0, n_limbs, 0, mod_begin, n_polys}, false);
 }
 int fhe_ntt_inv(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs) {
-  int rc = check_range(c, data, mod_begin, n_limbs);
+  int rc = check_range(c, data, mod_begin, n_limbs, n_polys);
   if (rc) return rc;
   return ntt_launch(c, LimbMap{data, n_limbs, n_limbs, 0, n_limbs, 0, mod_begin, n_polys}, true);
 }
 
 static int ew(fhe_ctx *c, EwOp op, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_polys,
               uint32_t mod_begin, uint32_t n_limbs) {
-  int rc = check_range(c, a, mod_begin, n_limbs);
+  int rc = check_range(c, a, mod_begin, n_limbs, n_polys);
   if (rc) return rc;
+  if (!n_polys) return FHE_OK;
   if (!b || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   return ew_launch(c, op, a, b, out, n_polys, mod_begin, n_limbs);
 }
@@ -414,7 +416,7 @@ int fhe_base_conv(fhe_ctx *c, const uint64_t *src, const uint32_t *src_mods, uin
 
 int fhe_fill_uniform(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs,
                      uint64_t seed) {
-  int rc = check_range(c, data, mod_begin, n_limbs);
+  int rc = check_range(c, data, mod_begin, n_limbs, n_polys);
   if (rc) return rc;
   return fill_uniform_launch(c, data, n_polys, mod_begin, n_limbs, seed);
 }
@@ -426,25 +428,25 @@ int fhe_sub(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uin
   return ew(c, EwOp::Sub, a, b, out, 2 * n_ct, 0, c ? c->L : 1);
 }
 
-static int need_ks(fhe_ctx *c, const void *a, const void *k, const void *out) {
+static int need_ks(fhe_ctx *c, const void *a, const void *k, const void *out, uint32_t n) {
   if (!c) return FHE_ERR_INVALID;
-  if (!a || !k || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   if (c->K == 0) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "context has no special primes (K = 0)");
+  if (n && (!a || !k || !out)) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   return FHE_OK;
 }
 
 int fhe_mul_relin(fhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk, uint64_t *out,
                   uint32_t n_ct) {
-  int rc = need_ks(c, a, rlk, out);
+  int rc = need_ks(c, a, rlk, out, n_ct);
   if (rc) return rc;
-  if (!b) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   if (!n_ct) return FHE_OK;
+  if (!b) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   if (c->params.scheme == FHE_SCHEME_BFV) return bfv_mul_relin_impl(c, a, b, rlk, out, n_ct);
   return ckks_mul_relin_impl(c, a, b, rlk, out, n_ct);
 }
 
 int fhe_keyswitch(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n) {
-  int rc = need_ks(c, d, ksk, out);
+  int rc = need_ks(c, d, ksk, out, n);
   if (rc) return rc;
   if (!n) return FHE_OK;
   void *ws;
@@ -453,7 +455,7 @@ int fhe_keyswitch(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *
 }
 
 int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out, uint32_t n_ct) {
-  int rc = need_ks(c, ct, gk, out);
+  int rc = need_ks(c, ct, gk, out, n_ct);
   if (rc) return rc;
   if ((g & 1) == 0 || g >= 2 * c->n) return fhe_fail(c, FHE_ERR_INVALID, "galois element must be odd and < 2N");
   if (!n_ct) return FHE_OK;

@@ -32,6 +32,8 @@
  *    /root/reference/src/execution/executor/executor.cpp:168-178).
  *  - calls on one context are serialised by the caller; work is enqueued on
  *    the context's stream (fhe_set_stream) and is asynchronous.
+ *  - a call over an empty batch (count 0) is a no-op and accepts null buffers
+ *    (the other arguments are still validated).
  */
 #ifndef HERDSMAN_PLUGINS_FHE_BACKEND_H
 #define HERDSMAN_PLUGINS_FHE_BACKEND_H

@@ -352,3 +352,68 @@ def test_errors_are_loud(hb):
         c.mul_relin(hb.empty((1, 2, 2, 1 << 12)), hb.empty((1, 2, 2, 1 << 12)), x, hb.empty((1, 2, 2, 1 << 12)))
     with pytest.raises(hb.FheBackendError):
         hb.Context(SCHEME_CKKS, 9, 2)  # N below the supported range
+
+
+# ------------------------------------------------------------ edge values
+def _edge_inputs(o, shape, seed):
+    """Residues at the boundaries of the Montgomery / lazy-reduction ranges:
+    0 (every partial product word zero: the folded carries must vanish), 1,
+    q-1, q-2 and 2^32-multiples (zero low words), mixed with uniform words."""
+    x = o.uniform(shape, seed=seed)
+    nl = shape[-2]
+    flat = x.reshape(-1, nl, shape[-1])
+    for li in range(nl):
+        q = int(o.moduli[li])
+        specials = np.array([0, 1, q - 1, q - 2, 1 << 32, (q - 1) & ~0xFFFFFFFF, q >> 1], dtype=np.uint64)
+        flat[:, li, : specials.size] = specials
+        flat[:, li, specials.size: 2 * specials.size] = specials[::-1]
+    flat[0, :, :] = 0  # one all-zero polynomial
+    return x
+
+
+@pytest.mark.parametrize("log_n,L", [(12, 3), (16, 4)])
+def test_ntt_edge_values(hb, log_n, L):
+    o, c = pair(hb, SCHEME_CKKS, log_n, L)
+    x = _edge_inputs(o, (3, L, 1 << log_n), seed=90)
+    d = hb.to_device(x)
+    c.ntt_fwd(d)
+    y = o.ntt_fwd(x.copy())
+    assert np.array_equal(hb.to_host(d), y)
+    c.ntt_inv(d)
+    assert np.array_equal(hb.to_host(d), x)
+
+
+@pytest.mark.parametrize("log_n", [12, 16])
+def test_ckks_mul_relin_edge_values(hb, log_n):
+    L, K, dnum = (5, 2, 3) if log_n == 12 else (12, 4, 3)
+    o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum)
+    a = _edge_inputs(o, (2, 2, L, 1 << log_n), seed=91)
+    b = _edge_inputs(o, (2, 2, L, 1 << log_n), seed=92)
+    b[1] = 0  # ct x zero ciphertext
+    rlk = o.uniform(o.key_shape(), seed=93)
+    want = o.mul_relin(a, b, rlk)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(rlk), dout)
+    assert np.array_equal(hb.to_host(dout), want)
+
+
+def test_bfv_mul_relin_edge_values(hb):
+    o, c = pair(hb, SCHEME_BFV, 13, 3, 2, 2, t=65537)
+    a = _edge_inputs(o, (2, 2, 3, 1 << 13), seed=94)
+    b = _edge_inputs(o, (2, 2, 3, 1 << 13), seed=95)
+    rlk = o.uniform(o.key_shape(), seed=96)
+    want = o.mul_relin(a, b, rlk)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(rlk), dout)
+    assert np.array_equal(hb.to_host(dout), want)
+
+
+def test_empty_batches_are_no_ops(hb):
+    o, c = pair(hb, SCHEME_CKKS, 12, 3, 2, 2)
+    z = hb.empty((0, 2, 3, 1 << 12))
+    k = hb.to_device(o.uniform(o.key_shape(), seed=97))
+    c.mul_relin(z, z, k, z)
+    c.rotate(z, c.galois_elt(1), k, z)
+    c.add(z, z, z)
+    c.keyswitch(hb.empty((0, 3, 1 << 12)), k, z)
+    c.ntt_fwd(hb.empty((0, 3, 1 << 12)))

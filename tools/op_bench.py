@@ -1,0 +1,47 @@
+"""Time one ciphertext op at a BASELINE config (GPU box), for rocprofv3 runs.
+
+    python tools/op_bench.py bfv_mul|ckks_mul|ckks_rot [--batch 32] [--reps 10]
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("op", choices=["bfv_mul", "ckks_mul", "ckks_rot"])
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+    import herdsman_amd.backend as hb
+
+    if args.op == "bfv_mul":
+        c = hb.Context(hb.SCHEME_BFV, 15, 8, 4, 2, t=65537)
+    else:
+        c = hb.Context(hb.SCHEME_CKKS, 16, 12, 4, 3)
+    s = torch.cuda.current_stream()
+    c.set_stream(s)
+    shape = (args.batch, 2, c.L, c.n)
+    a = c.fill_uniform(hb.empty(shape), seed=1)
+    b = c.fill_uniform(hb.empty(shape), seed=2)
+    k = c.fill_uniform(hb.empty(c.key_shape()), seed=3)
+    out = hb.empty(shape)
+    g = c.galois_elt(1)
+    fn = {"bfv_mul": lambda: c.mul_relin(a, b, k, out), "ckks_mul": lambda: c.mul_relin(a, b, k, out),
+          "ckks_rot": lambda: c.rotate(a, g, k, out)}[args.op]
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        fn()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.reps
+    print(f"{args.op}: {dt * 1e3:.3f} ms per call of {args.batch} -> {args.batch / dt:.1f} ops/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/roofline" -o run -- \
   python3 bench.py --roofline-only --no-cpu > "$OUT/roofline.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench" -o run -- \
-  python3 bench.py --steps 5 --warmup 2 --no-cpu > "$OUT/bench.log" 2>&1
+  python3 bench.py --steps 5 --warmup 2 --no-cpu --no-secondary > "$OUT/bench.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
   python3 bench.py --roofline-only --no-cpu > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
