@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline duration")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph", type=int, default=0, help="1: replay the step from a captured HIP graph")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary measurements (C4 rotate, C3 BFV mul+relin, C2 NTT)")
     ap.add_argument("--roofline-only", action="store_true",
@@ -96,6 +97,18 @@ def main():
 
     def step():
         ctx.mul_relin(a, b, rlk, out)
+
+    if args.graph and not args.roofline_only:
+        # capture one step (~25 kernel launches) into a HIP graph and replay it:
+        # the workspace was pre-sized by ctx.reserve, so nothing allocates
+        ctx.mul_relin(a, b, rlk, out)  # warm
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ctx.set_stream(torch.cuda.current_stream(dev))
+            ctx.mul_relin(a, b, rlk, out)
+        ctx.set_stream(stream)
+        step = graph.replay
 
     steps = 0 if args.roofline_only else args.steps
     for _ in range(0 if args.roofline_only else args.warmup):

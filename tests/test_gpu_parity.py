@@ -417,3 +417,30 @@ def test_empty_batches_are_no_ops(hb):
     c.add(z, z, z)
     c.keyswitch(hb.empty((0, 3, 1 << 12)), k, z)
     c.ntt_fwd(hb.empty((0, 3, 1 << 12)))
+
+
+def test_graph_capture_replay(hb):
+    """With the scratch pre-sized (fhe_reserve), a mul+relin step captures into a
+    HIP graph (torch.cuda.CUDAGraph) and its replays are bit-exact."""
+    import torch
+    o, c = pair(hb, SCHEME_CKKS, 13, 4, 2, 2)
+    a = o.uniform((3, 2, 4, 1 << 13), seed=100)
+    b = o.uniform((3, 2, 4, 1 << 13), seed=101)
+    rlk = o.uniform(o.key_shape(), seed=102)
+    want = o.mul_relin(a, b, rlk)
+    da, db, dk, dout = hb.to_device(a), hb.to_device(b), hb.to_device(rlk), hb.empty(a.shape)
+    c.reserve(3)
+    main = torch.cuda.current_stream()
+    c.set_stream(main)
+    c.mul_relin(da, db, dk, dout)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        c.set_stream(torch.cuda.current_stream())
+        c.mul_relin(da, db, dk, dout)
+    c.set_stream(main)
+    dout.zero_()
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(hb.to_host(dout), want)
