@@ -363,13 +363,18 @@ struct BehzDev {
 
 // behz_extend (oracle): fastbconv_m_tilde then sm_mrq.  x [L] coef -> [nB] coef
 template <int NL, bool SP>
-__global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__restrict__ xq, u64 *__restrict__ xb,
+// Poly p = 4 item + w of the BFV product's operands (w: a0, a1, b0, b1) is
+// read straight from the ciphertexts, copied into xq (the Q part the NTT then
+// transforms in place) and extended to Bsk in xb.
+__global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                               u64 *__restrict__ xq, u64 *__restrict__ xb,
                                                                const BehzDev *bz, const ModInfo *mods, u32 log_n) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const u32 p = blockIdx.y;
+  const u32 p = blockIdx.y, item = p >> 2, w = p & 3;
   const size_t N = (size_t)1 << log_n;
   const u32 L = bz->L, nB = bz->nB;
-  const u64 *s = xq + (size_t)p * L * N + k;
+  const u64 *s = (w < 2 ? a : b) + ((size_t)(2 * item + (w & 1)) * L) * N + k;
+  u64 *cq = xq + (size_t)p * L * N + k;
   u64 v[NL];
   u32 xmt = 0;
 #pragma unroll
@@ -377,7 +382,9 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
     v[i] = 0;
     if (i < (int)L) {
       const ModInfo m = mods[i];
-      v[i] = csub(mont_mul<SP>(s[i * N], bz->mt_hinv_R[i], m), m.q);
+      const u64 x = ld_nt(s + i * N);
+      cq[i * N] = x;
+      v[i] = csub(mont_mul<SP>(x, bz->mt_hinv_R[i], m), m.q);
       xmt += (u32)v[i] * bz->h_mod_mt[i];
     }
   }
@@ -536,12 +543,12 @@ int tensor_impl(fhe_ctx *c, const TensorArgs &t, u32 jobs) {
 }
 
 template <bool SP>
-int behz_extend_impl(fhe_ctx *c, const u64 *xq, u64 *xb, u32 polys) {
-  dim3 grid(c->n / EW_BLOCK, polys);
+int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xq, u64 *xb, u32 n) {
+  dim3 grid(c->n / EW_BLOCK, 4 * n);
   const BehzDev *bz = (const BehzDev *)c->behz;
-  if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, xq, xb, bz, c->d_mods, c->log_n);
-  else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, xq, xb, bz, c->d_mods, c->log_n);
-  else hipLaunchKernelGGL((behz_extend_kernel<24, SP>), grid, dim3(EW_BLOCK), 0, c->stream, xq, xb, bz, c->d_mods, c->log_n);
+  if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xq, xb, bz, c->d_mods, c->log_n);
+  else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xq, xb, bz, c->d_mods, c->log_n);
+  else hipLaunchKernelGGL((behz_extend_kernel<24, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xq, xb, bz, c->d_mods, c->log_n);
   return fhe_check(c, hipGetLastError(), "behz_extend");
 }
 
@@ -769,16 +776,9 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   u64 *eb = eq + (size_t)n * 3 * L * N;       // [n][3][nB][N]
   u64 *r2 = eb + (size_t)n * 3 * nB * N;      // [n][L][N]
   u64 *ksws = r2 + (size_t)n * L * N;
-  const size_t ct_words = (size_t)2 * L * N, LN = (size_t)L * N, BN = (size_t)nB * N;
-  // 1. gather a0,a1,b0,b1 per item
-  if ((rc = fhe_check(c, hipMemcpy2DAsync(xq, 4 * LN * 8, a, ct_words * 8, ct_words * 8, n,
-                                          hipMemcpyDeviceToDevice, c->stream), "bfv copy a")))
-    return rc;
-  if ((rc = fhe_check(c, hipMemcpy2DAsync(xq + ct_words, 4 * LN * 8, b, ct_words * 8, ct_words * 8, n,
-                                          hipMemcpyDeviceToDevice, c->stream), "bfv copy b")))
-    return rc;
-  // 2. extend to Bsk (coefficient form)
-  if ((rc = SP_DISPATCH(c, behz_extend_impl, c, xq, xb, n * 4))) return rc;
+  const size_t LN = (size_t)L * N, BN = (size_t)nB * N;
+  // 1-2. gather a0,a1,b0,b1 per item into xq and extend them to Bsk (coefficient form)
+  if ((rc = SP_DISPATCH(c, behz_extend_impl, c, a, b, xq, xb, n))) return rc;
   // 3. NTT in Q and Bsk
   if ((rc = ntt_launch(c, LimbMap{xq, L, L, 0, L, 0, 0, 4 * n}, false))) return rc;
   if ((rc = ntt_launch(c, LimbMap{xb, nB, nB, 0, nB, 0, bsk0, 4 * n}, false))) return rc;
