@@ -392,7 +392,8 @@ int fhe_poly_mul(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out
 int fhe_base_conv(fhe_ctx *c, const uint64_t *src, const uint32_t *src_mods, uint32_t n_src, uint64_t *dst,
                   const uint32_t *dst_mods, uint32_t n_dst, uint32_t n) {
   if (!c || !src || !dst || !src_mods || !dst_mods) return fhe_fail(c, FHE_ERR_INVALID, "null argument");
-  if (n_src == 0 || n_src > 16 || n_dst == 0) return fhe_fail(c, FHE_ERR_INVALID, "conversion sizes");
+  if (n_src == 0 || n_src > 16 || n_dst == 0 || n_dst > FHE_MAX_MODS)
+    return fhe_fail(c, FHE_ERR_INVALID, "conversion sizes");
   std::vector<u32> s(src_mods, src_mods + n_src), d(dst_mods, dst_mods + n_dst);
   for (u32 x : s)
     if (x >= c->nmod) return fhe_fail(c, FHE_ERR_INVALID, "modulus id");

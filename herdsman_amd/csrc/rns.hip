@@ -56,26 +56,64 @@ __global__ void __launch_bounds__(EW_BLOCK) fill_kernel(u64 *out, const ModInfo 
 }
 
 // --------------------------------------------------------- base conversion
+#define CONV_MAX_ND 48
+// Conversion tables of one workgroup's ConvTab staged in LDS once, so the
+// per-target loop of conv_store issues no dependent global/scalar loads.
+template <int NS>
+struct ConvLds {
+  u64 h[NS * CONV_MAX_ND];
+  u64 q[CONV_MAX_ND];
+  u64 aux[CONV_MAX_ND];  // q_hi (special) or -q^-1 (generic)
+  u32 dm[CONV_MAX_ND];
+};
+template <int NS, bool SP>
+__device__ __forceinline__ void conv_stage(ConvLds<NS> &sh, const ConvTab &t, const ModInfo *mods) {
+  for (u32 x = threadIdx.x; x < t.ns * t.nd; x += EW_BLOCK) sh.h[x] = t.h[x];
+  for (u32 x = threadIdx.x; x < t.nd; x += EW_BLOCK) {
+    const u32 dm = t.dst_mod[x];
+    const ModInfo mi = mods[dm];
+    sh.dm[x] = dm;
+    sh.q[x] = mi.q;
+    sh.aux[x] = SP ? mi.q_hi : mi.qinv_neg;
+  }
+}
+// y_m = sum_i v_i h[i][m] for every target m, streamed to out[slot(m) * N]
+// (slot = the target's modulus id when by_mod, else m)
+template <int NS, bool SP>
+__device__ __forceinline__ void conv_store(const ConvLds<NS> &sh, const u64 (&v)[NS], u32 ns, u32 nd, u64 *out,
+                                           size_t N, bool by_mod, u32 mod_base) {
+#pragma unroll 2
+  for (u32 m = 0; m < nd; ++m) {
+    ModInfo mi;
+    mi.q = sh.q[m];
+    mi.q_hi = (u32)sh.aux[m];
+    mi.qinv_neg = sh.aux[m];
+    st_nt(out + (by_mod ? sh.dm[m] - mod_base : m) * N, dot_mont<NS, SP>(v, sh.h + m, nd, ns, mi));
+  }
+}
+
 // conv_apply (oracle): v_i = [x_i (S/s_i)^-1]_{s_i};  y_m = sum_i v_i [S/s_i]_{d_m} mod d_m.
 template <int NS, bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) conv_kernel(const u64 *__restrict__ src, u32 src_stride,
                                                         u64 *__restrict__ dst, u32 dst_stride, ConvTab t,
                                                         const ModInfo *mods, u32 log_n) {
+  __shared__ ConvLds<NS> sh;
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 p = blockIdx.y;
   const size_t N = (size_t)1 << log_n;
+  conv_stage<NS, SP>(sh, t, mods);
   const u64 *s = src + (size_t)p * src_stride * N + k;
-  u64 *d = dst + (size_t)p * dst_stride * N + k;
   u64 v[NS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     v[i] = 0;
     if (i < (int)t.ns) {
       const ModInfo ms = mods[t.src_mod[i]];
-      v[i] = csub(mont_mul<SP>(s[i * N], t.hinv[i], ms), ms.q);
+      v[i] = csub(mont_mul<SP>(ld_nt(s + i * N), t.hinv[i], ms), ms.q);
     }
   }
-  for (u32 m = 0; m < t.nd; ++m) st_nt(d + m * N, dot_mont<NS, SP>(v, t.h + m, t.nd, t.ns, mods[t.dst_mod[m]]));
+  __syncthreads();
+  conv_store<NS, SP>(sh, v, t.ns, t.nd, dst + (size_t)p * dst_stride * N + k, N, false, 0);
 }
 
 // ModUp (keyswitch_one, oracle): every limb of Q u P outside digit j is the
@@ -85,29 +123,18 @@ __global__ void __launch_bounds__(EW_BLOCK) conv_kernel(const u64 *__restrict__ 
 // product needs a single reduction.  The conversion table of the digit and the
 // destination moduli are staged in LDS once per workgroup, so the per-target
 // loop issues no dependent global/scalar loads.
-#define MODUP_MAX_ND 48
 template <int NS, bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__ dc, u32 dc_stride,
                                                          u64 *__restrict__ ext, const ConvTab *tabs,
                                                          const ModInfo *mods, u32 QP, u32 alpha, u32 ndig,
                                                          u32 log_n) {
-  __shared__ u64 sh_h[NS * MODUP_MAX_ND];
-  __shared__ u64 sh_q[MODUP_MAX_ND];
-  __shared__ u64 sh_aux[MODUP_MAX_ND];  // q_hi (special) or -q^-1 (generic)
-  __shared__ u32 sh_dm[MODUP_MAX_ND];
+  __shared__ ConvLds<NS> sh;
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 ct = blockIdx.y / ndig, j = blockIdx.y % ndig;
   const size_t N = (size_t)1 << log_n;
   const u32 lo = j * alpha;
   const ConvTab t = tabs[j];
-  for (u32 x = threadIdx.x; x < t.ns * t.nd; x += EW_BLOCK) sh_h[x] = t.h[x];
-  for (u32 x = threadIdx.x; x < t.nd; x += EW_BLOCK) {
-    const u32 dm = t.dst_mod[x];
-    const ModInfo mi = mods[dm];
-    sh_dm[x] = dm;
-    sh_q[x] = mi.q;
-    sh_aux[x] = SP ? mi.q_hi : mi.qinv_neg;
-  }
+  conv_stage<NS, SP>(sh, t, mods);
   const u64 *s = dc + ((size_t)ct * dc_stride + lo) * N + k;
   u64 v[NS];
 #pragma unroll
@@ -119,14 +146,7 @@ __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__
     }
   }
   __syncthreads();
-  u64 *e = ext + ((size_t)(ct * ndig + j) * QP) * N + k;
-  for (u32 m = 0; m < t.nd; ++m) {
-    ModInfo mi;
-    mi.q = sh_q[m];
-    mi.q_hi = (u32)sh_aux[m];
-    mi.qinv_neg = sh_aux[m];
-    st_nt(e + sh_dm[m] * N, dot_mont<NS, SP>(v, sh_h + m, t.nd, t.ns, mi));
-  }
+  conv_store<NS, SP>(sh, v, t.ns, t.nd, ext + ((size_t)(ct * ndig + j) * QP) * N + k, N, true, 0);
 }
 
 // KS preparation for an input d (fhe_keyswitch, BFV): dc = d and the own-digit
