@@ -103,6 +103,37 @@ def test_no_gpu_task_fails_loudly(wg_run, tmp_path):
     assert r.returncode == 2 and "status: ERROR" in r.stdout
 
 
+# host sanitizers (ASan + UBSan on the adaptor; the HIP library is not instrumented)
+SAN_ENV = dict(os.environ, ASAN_OPTIONS="verify_asan_link_order=0:detect_leaks=1:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+
+
+@pytest.fixture(scope="module")
+def wg_run_san():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "herdsman_amd"), "sanitize"], check=True)
+    return os.path.join(ROOT, "herdsman_amd", "bin", "wg_run_san")
+
+
+def _clean(r):
+    out = r.stdout + r.stderr
+    return "AddressSanitizer" not in out and "runtime error" not in out and "LeakSanitizer" not in out
+
+
+def test_sanitized_completion_handoff(wg_run_san):
+    r = subprocess.run([wg_run_san, "race", "200"], capture_output=True, text=True, timeout=300, env=SAN_ENV)
+    assert r.returncode == 0 and _clean(r), r.stdout + r.stderr
+    assert "200/200 delivered" in r.stdout
+
+
+def test_sanitized_no_gpu_task(wg_run_san, tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    r = subprocess.run([wg_run_san, "map", str(tmp_path), str(tmp_path), "s", "0", "0,12,2,1,1,0", "in", "0", "out",
+                        "in0", "in0", "add"], capture_output=True, text=True, timeout=120, env=SAN_ENV)
+    assert r.returncode == 2 and "status: ERROR" in r.stdout and _clean(r), r.stdout + r.stderr
+
+
 # ---------------------------------------------------------------- GPU
 def _setup(tmp_path, scheme, log_n, L, K, dnum, t=0):
     from oracle_ffi import Oracle
