@@ -1,11 +1,9 @@
 // modarith.hpp -- 64-bit modular arithmetic for gfx950 (device) and host.
 //
-// gfx950 has no 64x64 multiplier: every u64 product is built from 32-bit
-// v_mad_u64_u32 / v_mul_hi_u32 / v_mul_lo_u32, all QUARTER rate
-// (tools/microbench/intops.hip: ~20 T lane-ops/s each vs 78.6 T for a
-// full-rate VALU op).  The multiply count per modular product is therefore
-// the figure of merit, and the backend is built on Montgomery arithmetic with
-// R = 2^64:
+// gfx950 has no 64x64 multiplier: every u64 product is built from 32x32->64
+// v_mad_u64_u32 (half the issue rate of a 32-bit add, tools/microbench/
+// valu64.hip), so the multiply count per modular product is the figure of
+// merit, and the backend is built on Montgomery arithmetic with R = 2^64:
 //   * mul128(a, b): the 128-bit product from exactly 4 v_mad_u64_u32;
 //   * mont_reduce(T) = T * 2^-64 mod q in [0, 2q) for T < q * 2^64:
 //       - "special" moduli q = 1 (mod 2^32) (the backend's default prime
