@@ -444,3 +444,23 @@ def test_graph_capture_replay(hb):
         g.replay()
     torch.cuda.synchronize()
     assert np.array_equal(hb.to_host(dout), want)
+
+
+@pytest.mark.parametrize("scheme,log_n,L,K,dnum", [(SCHEME_CKKS, 12, 32, 16, 2), (SCHEME_CKKS, 15, 20, 8, 5),
+                                                   (SCHEME_BFV, 12, 15, 4, 3)])
+def test_large_modulus_counts(hb, scheme, log_n, L, K, dnum):
+    """The widest shapes the context accepts: 48 moduli with 16-limb digits (ModUp/ModDown
+    NS=16 paths), 5 digits at a two-pass size, and BFV with a 16-modulus BEHZ base."""
+    t = 65537 if scheme == SCHEME_BFV else 0
+    o, c = pair(hb, scheme, log_n, L, K, dnum, t=t)
+    a = o.uniform((2, 2, L, 1 << log_n), seed=110)
+    b = o.uniform((2, 2, L, 1 << log_n), seed=111)
+    rlk = o.uniform(o.key_shape(), seed=112)
+    want = o.mul_relin(a, b, rlk)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(rlk), dout)
+    assert np.array_equal(hb.to_host(dout), want)
+    g = o.galois_elt(3)
+    want_r = o.rotate(a, g, rlk)
+    c.rotate(hb.to_device(a), g, hb.to_device(rlk), dout)
+    assert np.array_equal(hb.to_host(dout), want_r)
