@@ -198,3 +198,44 @@ def test_gpu_reduce_task_add_and_mul_trees(wg_run, tmp_path):
         comb = o.mul_relin(lo, hi, rlk)
         live = list(comb) + live[half:len(live) - half]
     assert np.array_equal(got, live[0])
+
+
+@pytest.mark.gpu
+def test_gpu_map_task_bfv(wg_run, tmp_path):
+    from oracle_ffi import SCHEME_BFV
+    o, storage, keys = _setup(tmp_path, SCHEME_BFV, 13, 3, 2, 2, t=65537)
+    rows = 3
+    a = o.uniform((rows, 2, o.L, o.n), seed=21)
+    b = o.uniform((rows, 2, o.L, o.n), seed=22)
+    rlk = o.uniform(o.key_shape(), seed=23)
+    write_partition(os.path.join(storage, "sb", "in", "0"), [ct_row(o, [a[i], b[i]]) for i in range(rows)])
+    write_keys(os.path.join(keys, "sb", "1.key"), o, rlk, {})
+    # (in0 * in1) + in0
+    r = subprocess.run([wg_run, "map", storage, keys, "sb", "1", params_arg(o, str(tmp_path)), "in", "0", "out",
+                        "in0", "in1", "mul", "in0", "add"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.stack([parse_row(o, p) for p in read_partition(os.path.join(storage, "sb", "out", "0"))])
+    assert np.array_equal(got, o.ct_add(o.mul_relin(a, b, rlk), a))
+
+
+@pytest.mark.gpu
+def test_gpu_bad_inputs_fail_the_task(wg_run, tmp_path):
+    """A key file for other moduli, or a truncated ciphertext row, ends the task with
+    Status::ERROR (no exception crosses the seam, nothing is written)."""
+    from oracle_ffi import Oracle, SCHEME_CKKS
+    o, storage, keys = _setup(tmp_path, SCHEME_CKKS, 12, 3, 2, 2)
+    other = Oracle(SCHEME_CKKS, 12, 3, 2, 2, moduli=np.concatenate([o.moduli[1:2], o.moduli[:1], o.moduli[2:]]))
+    a = o.uniform((1, 2, o.L, o.n), seed=31)[0]
+    write_partition(os.path.join(storage, "sx", "in", "0"), [ct_row(o, [a, a])])
+    write_keys(os.path.join(keys, "sx", "0.key"), other, o.uniform(o.key_shape(), seed=32), {})
+    base = [wg_run, "map", storage, keys, "sx", "0", params_arg(o, str(tmp_path)), "in", "0"]
+    r = subprocess.run(base + ["out1", "in0", "in1", "mul"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 2 and "status: ERROR" in r.stdout, r.stdout + r.stderr
+    assert not os.path.exists(os.path.join(storage, "sx", "out1", "0"))
+    row = ct_row(o, [a, a])
+    write_partition(os.path.join(storage, "sy", "in", "1"), [row[: len(row) - 8]])
+    write_keys(os.path.join(keys, "sy", "0.key"), o, o.uniform(o.key_shape(), seed=33), {})
+    r = subprocess.run([wg_run, "map", storage, keys, "sy", "0", params_arg(o, str(tmp_path)), "in", "1", "out2",
+                        "in0", "in1", "mul"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 2 and "status: ERROR" in r.stdout, r.stdout + r.stderr
+    assert not os.path.exists(os.path.join(storage, "sy", "out2", "1"))
