@@ -162,19 +162,33 @@ HD u64 reduce128(U128 T, const ModInfo &m) {
   return csub(mont_mul<SP>(mont_reduce<SP>(T, m), m.r2, m), m.q);
 }
 
-// sum_{i < ns} v[i] * h[i * hs] mod m, exact, given canonical v[i] and
-// R-pre-scaled constants h.  Chunks of 4 keep each 128-bit sum < q * 2^64.
+// sum_{i < ns} v[i] * h[i * hs] * R^-1 mod m, exact and canonical, given
+// canonical v[i] and constants h[i] < m (pre-scaled by the caller's power of R).
+// Chunks of 4 terms:
+//  - special moduli: one Montgomery product per term (each < 2m, so a chunk
+//    sums below 8m < 2^64) and a 3-step conditional subtraction -- no 128-bit
+//    carry chains (tools/microbench/dot.hip: 1.35x the 128-bit form);
+//  - generic moduli: 128-bit sum (< q 2^64) and one Montgomery reduction.
 template <int NS, bool SP>
 HD u64 dot_mont(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
   u64 res = 0;
 #pragma unroll
   for (int c0 = 0; c0 < NS; c0 += 4) {
     if (c0 < (int)ns) {
-      U128 acc{0, 0};
+      u64 part;
+      if (SP) {
+        u64 sum = 0;
 #pragma unroll
-      for (int i = c0; i < c0 + 4 && i < NS; ++i)
-        if (i < (int)ns) mac128(acc, v[i], h[(size_t)i * hs]);
-      const u64 part = csub(mont_reduce<SP>(acc, m), m.q);
+        for (int i = c0; i < c0 + 4 && i < NS; ++i)
+          if (i < (int)ns) sum += mont_mul<SP>(v[i], h[(size_t)i * hs], m);
+        part = csub(csub(csub(sum, 4 * m.q), 2 * m.q), m.q);
+      } else {
+        U128 acc{0, 0};
+#pragma unroll
+        for (int i = c0; i < c0 + 4 && i < NS; ++i)
+          if (i < (int)ns) mac128(acc, v[i], h[(size_t)i * hs]);
+        part = csub(mont_reduce<SP>(acc, m), m.q);
+      }
       res = c0 == 0 ? part : add_mod(res, part, m.q);
     }
   }

@@ -82,7 +82,7 @@ __device__ __forceinline__ void conv_stage(ConvLds<NS> &sh, const ConvTab &t, co
 template <int NS, bool SP>
 __device__ __forceinline__ void conv_store(const ConvLds<NS> &sh, const u64 (&v)[NS], u32 ns, u32 nd, u64 *out,
                                            size_t N, bool by_mod, u32 mod_base) {
-#pragma unroll 2
+#pragma unroll 1
   for (u32 m = 0; m < nd; ++m) {
     ModInfo mi;
     mi.q = sh.q[m];
