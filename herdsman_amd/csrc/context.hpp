@@ -11,6 +11,14 @@
 #define FHE_MAX_MODS 48
 #define FHE_MAX_CONV_SRC 16
 
+// gridDim.y of the per-coefficient kernels holds (item, limb); every launch
+// keeps it below this bound
+constexpr u32 kMaxGridY = 65535;
+// ciphertext ops run over batches of at most this many ciphertexts per internal
+// pass: every grid's y-dimension stays below kMaxGridY (2 L <= 94 rows per
+// ciphertext) and the key-switch scratch stays bounded (29 GiB at N=2^16, L=12)
+constexpr u32 kCtChunk = 512;
+
 // A batch of limb-polynomials inside a [poly][poly_stride][N] buffer: active
 // limb a of poly p is limb `first + (a < skip_lo ? a : a + skip_len)` and uses
 // modulus `mod_offset + limb`.  Covers whole polys, Q- or P-parts and the
@@ -94,7 +102,6 @@ int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, 
 int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n, bool ntt_form);
 int tensor_launch(fhe_ctx *c, const u64 *a, size_t a_ct, size_t a_poly, const u64 *b, size_t b_ct, size_t b_poly,
                   u64 *e01, size_t e_ct, size_t e_poly, u64 *e2, size_t e2_ct, u32 n_ct, u32 nl, u32 mod_offset);
-int automorph_launch(fhe_ctx *c, const u64 *in, u64 *out, u32 g, u32 n_polys, bool ntt_form);
 int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n_ct);
 int behz_setup(fhe_ctx *c);
 size_t keyswitch_ws_bytes(const fhe_ctx *c, u32 n);

@@ -326,6 +326,7 @@ int fhe_synchronize(fhe_ctx *c) {
 
 int fhe_reserve(fhe_ctx *c, uint32_t max_batch) {
   if (!c) return FHE_ERR_INVALID;
+  max_batch = std::min(max_batch, kCtChunk);  // ops run in passes of at most kCtChunk ciphertexts
   size_t need = (size_t)sizeof(u64) * c->n * max_batch * 2 * c->L;  // rotate / mul scratch
   if (c->K) need += keyswitch_ws_bytes(c, max_batch);
   if (c->nB) need = std::max(need, bfv_mul_ws_bytes(c, max_batch));
@@ -442,8 +443,15 @@ int fhe_mul_relin(fhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64
   if (rc) return rc;
   if (!n_ct) return FHE_OK;
   if (!b) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
-  if (c->params.scheme == FHE_SCHEME_BFV) return bfv_mul_relin_impl(c, a, b, rlk, out, n_ct);
-  return ckks_mul_relin_impl(c, a, b, rlk, out, n_ct);
+  const size_t cw = (size_t)2 * c->L * c->n;
+  for (uint32_t c0 = 0; c0 < n_ct; c0 += kCtChunk) {
+    const uint32_t m = std::min(kCtChunk, n_ct - c0);
+    const size_t o = c0 * cw;
+    rc = c->params.scheme == FHE_SCHEME_BFV ? bfv_mul_relin_impl(c, a + o, b + o, rlk, out + o, m)
+                                            : ckks_mul_relin_impl(c, a + o, b + o, rlk, out + o, m);
+    if (rc) return rc;
+  }
+  return FHE_OK;
 }
 
 int fhe_keyswitch(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n) {
@@ -451,8 +459,15 @@ int fhe_keyswitch(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *
   if (rc) return rc;
   if (!n) return FHE_OK;
   void *ws;
-  if ((rc = ctx_workspace(c, keyswitch_ws_bytes(c, n), &ws))) return rc;
-  return keyswitch_ex(c, d, c->L, ksk, out, out, n, 0u, c->params.scheme == FHE_SCHEME_CKKS, (u64 *)ws);
+  if ((rc = ctx_workspace(c, keyswitch_ws_bytes(c, std::min(n, kCtChunk)), &ws))) return rc;
+  const size_t LN = (size_t)c->L * c->n;
+  for (uint32_t c0 = 0; c0 < n; c0 += kCtChunk) {
+    const uint32_t m = std::min(kCtChunk, n - c0);
+    rc = keyswitch_ex(c, d + c0 * LN, c->L, ksk, out + c0 * 2 * LN, out + c0 * 2 * LN, m, 0u,
+                      c->params.scheme == FHE_SCHEME_CKKS, (u64 *)ws);
+    if (rc) return rc;
+  }
+  return FHE_OK;
 }
 
 int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out, uint32_t n_ct) {
@@ -460,7 +475,12 @@ int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, u
   if (rc) return rc;
   if ((g & 1) == 0 || g >= 2 * c->n) return fhe_fail(c, FHE_ERR_INVALID, "galois element must be odd and < 2N");
   if (!n_ct) return FHE_OK;
-  return rotate_impl(c, ct, g, gk, out, n_ct, c->params.scheme == FHE_SCHEME_CKKS);
+  const size_t cw = (size_t)2 * c->L * c->n;
+  for (uint32_t c0 = 0; c0 < n_ct; c0 += kCtChunk) {
+    const uint32_t m = std::min(kCtChunk, n_ct - c0);
+    if ((rc = rotate_impl(c, ct + c0 * cw, g, gk, out + c0 * cw, m, c->params.scheme == FHE_SCHEME_CKKS))) return rc;
+  }
+  return FHE_OK;
 }
 
 int fhe_galois_elt(const fhe_ctx *c, int32_t steps, uint32_t *out) {

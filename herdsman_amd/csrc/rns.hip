@@ -47,9 +47,9 @@ __global__ void __launch_bounds__(EW_BLOCK) ew_kernel(const u64 *__restrict__ a,
 
 // orc_fill_uniform
 __global__ void __launch_bounds__(EW_BLOCK) fill_kernel(u64 *out, const ModInfo *mods, u32 mod_begin, u32 n_limbs,
-                                                        u32 log_n, u64 seed) {
+                                                        u32 log_n, u64 seed, u32 job0) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const u32 job = blockIdx.y;
+  const u32 job = job0 + blockIdx.y;  // the stream index is global over chunked launches
   const u64 q = mods[mod_begin + job % n_limbs].q;
   const size_t w = ((size_t)job << log_n) + k;
   out[w] = mulhi64(stream_word(seed, w), q);
@@ -327,38 +327,6 @@ __global__ void __launch_bounds__(EW_BLOCK) automorph_ks_kernel(const u64 *__res
   ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub(mont_mul<SP>(y1, m.r2, m), m.q);
 }
 
-// NTT-domain automorphism (orc_automorph_ntt): slot k holds a(psi^(2brv(k)+1))
-__global__ void __launch_bounds__(EW_BLOCK) automorph_ntt_kernel(const u64 *__restrict__ in, u64 *__restrict__ out,
-                                                                 u32 g, u32 log_n) {
-  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const size_t base = (size_t)blockIdx.y << log_n;
-  const u32 mask = (2u << log_n) - 1;
-  const u32 e = 2 * (__brev(k) >> (32 - log_n)) + 1;
-  const u32 e2 = (u32)(((u64)e * g) & mask);
-  const u32 src = __brev((e2 - 1) >> 1) >> (32 - log_n);
-  out[base + k] = in[base + src];
-}
-
-// coefficient-domain automorphism (orc_automorph_coef) as a gather:
-// out[d] = a[j0] if j0 < N else -a[j0 - N], j0 = d * g^-1 mod 2N
-__global__ void __launch_bounds__(EW_BLOCK) automorph_coef_kernel(const u64 *__restrict__ in, u64 *__restrict__ out,
-                                                                  u32 ginv, const ModInfo *mods, u32 n_limbs,
-                                                                  u32 log_n) {
-  const u32 d = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const size_t base = (size_t)blockIdx.y << log_n;
-  const u32 n = 1u << log_n, mask = 2 * n - 1;
-  const u32 j0 = (u32)(((u64)d * ginv) & mask);
-  u64 v;
-  if (j0 < n) {
-    v = in[base + j0];
-  } else {
-    const u64 q = mods[blockIdx.y % n_limbs].q;
-    const u64 x = in[base + j0 - n];
-    v = x ? q - x : 0;
-  }
-  out[base + d] = v;
-}
-
 // ----------------------------------------------------------------- BEHZ
 // Constants for SEAL-style BEHZ (behz_init in the oracle), Montgomery
 // pre-scaled ("_R" = times 2^64 mod the modulus it is used with).
@@ -588,24 +556,42 @@ int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *o
 
 // =================================================================== host
 
+// The per-coefficient kernels put (item, limb) on gridDim.y (< 2^16): larger
+// batches are issued as several launches over whole polys.
+static u32 polys_per_launch(u32 n_limbs) { return std::max<u32>(1, kMaxGridY / std::max<u32>(1, n_limbs)); }
+
 int ew_launch(fhe_ctx *c, EwOp op, const u64 *a, const u64 *b, u64 *out, u32 n_polys, u32 mod_begin, u32 n_limbs) {
-  const u32 jobs = n_polys * n_limbs;
-  if (!jobs) return FHE_OK;
-  return SP_DISPATCH(c, ew_impl, c, op, a, b, out, jobs, mod_begin, n_limbs);
+  const u32 per = polys_per_launch(n_limbs);
+  for (u32 p0 = 0; p0 < n_polys; p0 += per) {
+    const u32 np = std::min(per, n_polys - p0);
+    const size_t off = (size_t)p0 * n_limbs * c->n;
+    const int rc = SP_DISPATCH(c, ew_impl, c, op, a + off, b + off, out + off, np * n_limbs, mod_begin, n_limbs);
+    if (rc) return rc;
+  }
+  return FHE_OK;
 }
 
 int fill_uniform_launch(fhe_ctx *c, u64 *data, u32 n_polys, u32 mod_begin, u32 n_limbs, u64 seed) {
-  const u32 jobs = n_polys * n_limbs;
-  if (!jobs) return FHE_OK;
-  hipLaunchKernelGGL(fill_kernel, dim3(c->n / EW_BLOCK, jobs), dim3(EW_BLOCK), 0, c->stream, data, c->d_mods,
-                     mod_begin, n_limbs, c->log_n, seed);
-  return fhe_check(c, hipGetLastError(), "fill_kernel");
+  const u32 per = polys_per_launch(n_limbs);
+  for (u32 p0 = 0; p0 < n_polys; p0 += per) {
+    const u32 np = std::min(per, n_polys - p0);
+    hipLaunchKernelGGL(fill_kernel, dim3(c->n / EW_BLOCK, np * n_limbs), dim3(EW_BLOCK), 0, c->stream, data,
+                       c->d_mods, mod_begin, n_limbs, c->log_n, seed, p0 * n_limbs);
+    const int rc = fhe_check(c, hipGetLastError(), "fill_kernel");
+    if (rc) return rc;
+  }
+  return FHE_OK;
 }
 
 int conv_launch(fhe_ctx *c, const ConvTab &t, const u64 *src, u32 src_poly_stride, u64 *dst, u32 dst_poly_stride,
                 u32 n) {
-  if (!n) return FHE_OK;
-  return SP_DISPATCH(c, conv_impl, c, t, src, src_poly_stride, dst, dst_poly_stride, n);
+  for (u32 p0 = 0; p0 < n; p0 += kMaxGridY) {
+    const u32 np = std::min(kMaxGridY, n - p0);
+    const int rc = SP_DISPATCH(c, conv_impl, c, t, src + (size_t)p0 * src_poly_stride * c->n, src_poly_stride,
+                               dst + (size_t)p0 * dst_poly_stride * c->n, dst_poly_stride, np);
+    if (rc) return rc;
+  }
+  return FHE_OK;
 }
 
 size_t keyswitch_ws_bytes(const fhe_ctx *c, u32 n) {
@@ -699,22 +685,6 @@ int tensor_launch(fhe_ctx *c, const u64 *a, size_t a_ct, size_t a_poly, const u6
                   u64 *e01, size_t e_ct, size_t e_poly, u64 *e2, size_t e2_ct, u32 n_ct, u32 nl, u32 mod_offset) {
   TensorArgs t{a, b, e01, e2, a_ct, a_poly, b_ct, b_poly, e_ct, e_poly, e2_ct, nl, mod_offset, c->log_n};
   return SP_DISPATCH(c, tensor_impl, c, t, n_ct * nl);
-}
-
-int automorph_launch(fhe_ctx *c, const u64 *in, u64 *out, u32 g, u32 n_polys, bool ntt_form) {
-  const u32 jobs = n_polys * c->L;
-  if (ntt_form) {
-    hipLaunchKernelGGL(automorph_ntt_kernel, dim3(c->n / EW_BLOCK, jobs), dim3(EW_BLOCK), 0, c->stream, in, out, g,
-                       c->log_n);
-  } else {
-    // g^-1 mod 2N (g odd): Newton iteration on the 2-adic inverse
-    u32 inv = g;
-    for (int i = 0; i < 5; ++i) inv *= 2u - g * inv;
-    inv &= (2u * c->n) - 1;
-    hipLaunchKernelGGL(automorph_coef_kernel, dim3(c->n / EW_BLOCK, jobs), dim3(EW_BLOCK), 0, c->stream, in, out,
-                       inv, c->d_mods, c->L, c->log_n);
-  }
-  return fhe_check(c, hipGetLastError(), "automorph_kernel");
 }
 
 // ------------------------------------------------------------ BEHZ setup

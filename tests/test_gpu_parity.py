@@ -464,3 +464,26 @@ def test_large_modulus_counts(hb, scheme, log_n, L, K, dnum):
     want_r = o.rotate(a, g, rlk)
     c.rotate(hb.to_device(a), g, hb.to_device(rlk), dout)
     assert np.array_equal(hb.to_host(dout), want_r)
+
+
+def test_large_batches_are_chunked(hb):
+    """Batches beyond one launch's grid (2^16 (item, limb) rows) and beyond one
+    internal ciphertext pass (kCtChunk = 512) give the same bits as the oracle."""
+    o, c = pair(hb, SCHEME_CKKS, 10, 2, 1, 1)
+    n_big = 20000  # 2 * 20000 * 2 = 80000 (item, limb) rows
+    a = o.uniform((n_big, 2, 2, 1 << 10), seed=120)
+    b = o.uniform((n_big, 2, 2, 1 << 10), seed=121)
+    da = c.fill_uniform(hb.empty(a.shape), seed=120)
+    assert np.array_equal(hb.to_host(da), a)
+    dout = hb.empty(a.shape)
+    c.add(da, hb.to_device(b), dout)
+    assert np.array_equal(hb.to_host(dout), o.ct_add(a, b))
+    n = 600
+    rlk = o.uniform(o.key_shape(), seed=122)
+    want = o.mul_relin(a[:n], b[:n], rlk)
+    dout = hb.empty((n, 2, 2, 1 << 10))
+    c.mul_relin(hb.to_device(a[:n]), hb.to_device(b[:n]), hb.to_device(rlk), dout)
+    assert np.array_equal(hb.to_host(dout), want)
+    g = o.galois_elt(5)
+    c.rotate(hb.to_device(a[:n]), g, hb.to_device(rlk), dout)
+    assert np.array_equal(hb.to_host(dout), o.rotate(a[:n], g, rlk))
