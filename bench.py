@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32, help="ct-mults per GPU per step")
+    ap.add_argument("--batch", type=int, default=128, help="ct-mults per GPU per step")
     ap.add_argument("--ntt-reps", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=4096, help="max ct-mults in the CPU baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline duration")

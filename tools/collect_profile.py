@@ -61,8 +61,15 @@ def main(src, dst):
             valu_busy[k] = mean["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (mean["GRBM_GUI_ACTIVE"] / 8)
     fetch_b = sum(sum(v) / len(v) for v in fetch.values()) * 1024 * 2
     write_b = sum(sum(v) / len(v) for v in write.values()) * 1024
-    # bench.py --roofline-only: 32 ciphertexts x 3 digits x 12 limbs per fhe_ntt_fwd launch
-    limbs = 32 * 3 * L
+    # bench.py --roofline-only: batch x 3 digits x 12 limbs per fhe_ntt_fwd launch
+    batch = 32
+    try:
+        for line in open(f"{src}/roofline.log"):
+            if line.startswith("{"):
+                batch = json.loads(line)["config"]["batch_per_gpu"]
+    except (OSError, ValueError, KeyError):
+        pass
+    limbs = batch * 3 * L
     per_limb = (fetch_b + write_b) / limbs
     with open(f"{dst}/ntt_pmc.csv", "w", newline="") as fh:
         w = csv.DictWriter(fh, fieldnames=["kernel", "counter", "value", "grid"])
