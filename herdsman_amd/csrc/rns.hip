@@ -169,8 +169,9 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_prep_kernel(const u64 *__restrict
 //   acc_b[i] = sum_j ext_j[i] * ksk[j][b][i]  mod m_i,  b in {0,1}
 // One thread owns (limb i, coefficient k) for the WHOLE batch: the 2*dnum
 // key words are loaded once and reused by every ciphertext, so the 48 MiB key
-// is read once per call instead of once per ciphertext.  ext carries a factor
-// R, removed by the one Montgomery reduction per 4-term chunk.
+// is read once per call instead of once per ciphertext (up to 16 digits; more
+// digits stream the key words with the digits).  ext carries a factor R, which
+// the Montgomery products of dot_mont remove.
 template <bool SP, int MAXD>
 __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restrict__ ext, const u64 *__restrict__ ksk,
                                                             u64 *__restrict__ acc, const ModInfo *mods, u32 QP,
@@ -179,41 +180,46 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restric
   const u32 i = blockIdx.y;
   const size_t N = (size_t)1 << log_n;
   const ModInfo m = mods[i];
-  u64 k0[MAXD], k1[MAXD];
-#pragma unroll
-  for (int j = 0; j < MAXD; ++j) {
-    if (j < (int)ndig) {
-      k0[j] = ksk[((size_t)(2 * j) * QP + i) * N + k];
-      k1[j] = ksk[((size_t)(2 * j + 1) * QP + i) * N + k];
-    }
-  }
   const size_t ext_ct = (size_t)ndig * QP * N, acc_ct = (size_t)2 * QP * N;
   const u64 *e = ext + (size_t)i * N + k;
   u64 *o = acc + (size_t)i * N + k;
-#pragma unroll 2
-  for (u32 ct = 0; ct < n_ct; ++ct) {
-    u64 x[MAXD];
+  const u64 *kp = ksk + (size_t)i * N + k;  // key word (j, b) at kp[(2 j + b) QP N]
+  if constexpr (MAXD > 0) {
+    // the 2 ndig key words of this coefficient stay in registers for the whole batch
+    u64 k0[MAXD], k1[MAXD];
 #pragma unroll
-    for (int j = 0; j < MAXD; ++j)
-      if (j < (int)ndig) x[j] = ld_nt(e + ct * ext_ct + (size_t)j * QP * N);
-    u64 r0 = 0, r1 = 0;
-#pragma unroll
-    for (int j0 = 0; j0 < MAXD; j0 += 4) {
-      if (j0 < (int)ndig) {
-        U128 a0{0, 0}, a1{0, 0};
-#pragma unroll
-        for (int j = j0; j < j0 + 4 && j < MAXD; ++j) {
-          if (j < (int)ndig) {
-            mac128(a0, x[j], k0[j]);
-            mac128(a1, x[j], k1[j]);
-          }
-        }
-        r0 = add_mod(r0, csub(mont_reduce<SP>(a0, m), m.q), m.q);
-        r1 = add_mod(r1, csub(mont_reduce<SP>(a1, m), m.q), m.q);
-      }
+    for (int j = 0; j < MAXD; ++j) {
+      k0[j] = j < (int)ndig ? kp[(size_t)(2 * j) * QP * N] : 0;
+      k1[j] = j < (int)ndig ? kp[(size_t)(2 * j + 1) * QP * N] : 0;
     }
-    st_nt(o + ct * acc_ct, r0);
-    st_nt(o + ct * acc_ct + (size_t)QP * N, r1);
+#pragma unroll 1
+    for (u32 ct = 0; ct < n_ct; ++ct) {
+      u64 x[MAXD];
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) x[j] = j < (int)ndig ? ld_nt(e + ct * ext_ct + (size_t)j * QP * N) : 0;
+      st_nt(o + ct * acc_ct, dot_mont<MAXD, SP>(x, k0, 1, ndig, m));
+      st_nt(o + ct * acc_ct + (size_t)QP * N, dot_mont<MAXD, SP>(x, k1, 1, ndig, m));
+    }
+  } else {
+    // many digits (> 16): stream the key words with the digits, 4 at a time
+    for (u32 ct = 0; ct < n_ct; ++ct) {
+      u64 r0 = 0, r1 = 0;
+      for (u32 j0 = 0; j0 < ndig; j0 += 4) {
+        u64 x[4], h0[4], h1[4];
+        const u32 nj = ndig - j0 < 4 ? ndig - j0 : 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool on = j < (int)nj;
+          x[j] = on ? ld_nt(e + ct * ext_ct + (size_t)(j0 + j) * QP * N) : 0;
+          h0[j] = on ? kp[(size_t)(2 * (j0 + j)) * QP * N] : 0;
+          h1[j] = on ? kp[(size_t)(2 * (j0 + j) + 1) * QP * N] : 0;
+        }
+        r0 = add_mod(r0, dot_mont<4, SP>(x, h0, 1, nj, m), m.q);
+        r1 = add_mod(r1, dot_mont<4, SP>(x, h1, 1, nj, m), m.q);
+      }
+      st_nt(o + ct * acc_ct, r0);
+      st_nt(o + ct * acc_ct + (size_t)QP * N, r1);
+    }
   }
 }
 
@@ -480,8 +486,10 @@ int inner_impl(fhe_ctx *c, const u64 *ext, const u64 *ksk, u64 *acc, u32 n, u32 
     hipLaunchKernelGGL((ks_inner_kernel<SP, 4>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
   else if (ndig <= 8)
     hipLaunchKernelGGL((ks_inner_kernel<SP, 8>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
+  else if (ndig <= 16)
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 16>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
   else
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 48>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 0>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
   return fhe_check(c, hipGetLastError(), "ks_inner_kernel");
 }
 
