@@ -18,7 +18,9 @@ SCHEME_CKKS = 0
 SCHEME_BFV = 1
 
 FHE_OK = 0
-_ERRORS = {-1: "FHE_ERR_INVALID", -2: "FHE_ERR_DEVICE", -3: "FHE_ERR_OOM", -4: "FHE_ERR_UNSUPPORTED"}
+FHE_ERR_INVALID, FHE_ERR_DEVICE, FHE_ERR_OOM, FHE_ERR_UNSUPPORTED = -1, -2, -3, -4
+_ERRORS = {FHE_ERR_INVALID: "FHE_ERR_INVALID", FHE_ERR_DEVICE: "FHE_ERR_DEVICE", FHE_ERR_OOM: "FHE_ERR_OOM",
+           FHE_ERR_UNSUPPORTED: "FHE_ERR_UNSUPPORTED"}
 
 
 class FheBackendError(RuntimeError):

@@ -489,3 +489,34 @@ def test_large_batches_are_chunked(hb):
     g = o.galois_elt(5)
     c.rotate(hb.to_device(a[:n]), g, hb.to_device(rlk), dout)
     assert np.array_equal(hb.to_host(dout), o.rotate(a[:n], g, rlk))
+
+
+def test_rccl_entry_points_single_rank(hb):
+    """fhe_bcast_key and fhe_reduce_ranks on a real one-rank RCCL communicator (the
+    box has one GPU): the calls go through RCCL and leave the data as it is."""
+    import ctypes as C
+    import torch
+    # the communicator must come from the RCCL instance libherdsman_fhe.so bound to:
+    # in a process that imported torch that is torch's bundled librccl.so.1, which a
+    # soname lookup returns (a second copy would see a "corrupted comm object")
+    hb.load_library()
+    rccl = C.CDLL("librccl.so.1")
+    comm = C.c_void_p()
+    dev = (C.c_int * 1)(0)
+    assert rccl.ncclCommInitAll(C.byref(comm), 1, dev) == 0
+    try:
+        o, c = pair(hb, SCHEME_CKKS, 12, 3, 2, 2)
+        key = o.uniform(o.key_shape(), seed=130)
+        dk = hb.to_device(key)
+        lib = hb.load_library()
+        rc = lib.fhe_bcast_key(c.h, dk.data_ptr(), key.size, comm, 0)
+        assert rc == 0, lib.fhe_last_error(c.h)
+        ct = o.uniform((1, 2, 3, 1 << 12), seed=131)
+        dct, tmp = hb.to_device(ct), hb.empty(ct.shape)
+        assert lib.fhe_reduce_ranks(c.h, dct.data_ptr(), hb.REDUCE_ADD, None, comm, 0, tmp.data_ptr()) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(hb.to_host(dk), key)
+        assert np.array_equal(hb.to_host(dct), ct)
+        assert lib.fhe_reduce_ranks(c.h, dct.data_ptr(), 7, None, comm, 0, tmp.data_ptr()) == hb.FHE_ERR_INVALID
+    finally:
+        rccl.ncclCommDestroy(comm)
