@@ -520,3 +520,16 @@ def test_rccl_entry_points_single_rank(hb):
         assert lib.fhe_reduce_ranks(c.h, dct.data_ptr(), 7, None, comm, 0, tmp.data_ptr()) == hb.FHE_ERR_INVALID
     finally:
         rccl.ncclCommDestroy(comm)
+
+
+@pytest.mark.parametrize("scheme", [SCHEME_CKKS, SCHEME_BFV])
+def test_conjugation_and_identity_galois(hb, scheme):
+    """Galois elements 2N-1 (conjugation) and 1 (identity automorphism + key switch)."""
+    t = 65537 if scheme == SCHEME_BFV else 0
+    o, c = pair(hb, scheme, 12, 4, 2, 2, t=t)
+    ct = o.uniform((2, 2, 4, 1 << 12), seed=140)
+    gk = o.uniform(o.key_shape(), seed=141)
+    dout = hb.empty(ct.shape)
+    for g in (2 * o.n - 1, 1):
+        c.rotate(hb.to_device(ct), g, hb.to_device(gk), dout)
+        assert np.array_equal(hb.to_host(dout), o.rotate(ct, g, gk)), g
