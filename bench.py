@@ -67,12 +67,19 @@ def main():
     from herdsman_amd.dist import world as dist_world
 
     rank, local, world = dist_world()
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # HERD_BENCH_DIST=gloo rehearses the multi-rank control flow with several ranks
+    # sharing the GPUs there are (the real runs use RCCL, one rank per GPU)
+    backend = os.environ.get("HERD_BENCH_DIST", "nccl")
+    gpu = local % torch.cuda.device_count() if backend == "gloo" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
-    ctx = hb.Context(hb.SCHEME_CKKS, LOG_N, L, K, DNUM, device=local)
+    ctx = hb.Context(hb.SCHEME_CKKS, LOG_N, L, K, DNUM, device=gpu)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream)
     n = 1 << LOG_N

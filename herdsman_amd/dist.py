@@ -29,11 +29,22 @@ def shard_range(total: int, world_size: int, rank: int) -> Tuple[int, int]:
     return begin, begin + base + (1 if rank < extra else 0)
 
 
+def _host_staged() -> bool:
+    """gloo moves host tensors only: device tensors are staged through host memory."""
+    import torch.distributed as dist
+    return dist.get_backend() == "gloo"
+
+
 def broadcast_key(key, src: int = 0) -> None:
     """Broadcast an evaluation key tensor in place (the only collective)."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.broadcast(key, src=src)
+        if key.is_cuda and _host_staged():
+            tmp = key.cpu()
+            dist.broadcast(tmp, src=src)
+            key.copy_(tmp)
+        else:
+            dist.broadcast(key, src=src)
 
 
 def max_over_ranks(x: float, device=None) -> float:
@@ -42,7 +53,7 @@ def max_over_ranks(x: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=None if _host_staged() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
