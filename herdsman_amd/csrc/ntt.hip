@@ -2,7 +2,8 @@
 //
 // Algorithm (same transform as the oracle's orc_ntt_fwd, oracle/fhe_oracle.c):
 // Harvey's lazy Cooley-Tukey forward (natural in, bit-reversed out, values in
-// [0,4q) between stages) and Gentleman-Sande inverse ([0,2q)).  The twiddle of
+// [0,4q) between stages, or [0,8q) with fewer reductions for q < 2^60 -- see
+// wide_csub) and Gentleman-Sande inverse ([0,2q)).  The twiddle of
 // butterfly (j, j+t) at global stage s is psi^brv(2^s + (j >> (logN - s))),
 // stored in Montgomery form (psi^e * 2^64 mod q) so one mont_mul = 6
 // quarter-rate multiplies gives the exact product (modarith.hpp).
@@ -15,6 +16,8 @@
 //   N  = 2^15..2^17 : two passes (column pass of stride N/2^S1, then row pass
 //               of contiguous 2^S2 blocks), because a 512 KiB N=2^16 residue
 //               exceeds the 160 KiB LDS of a CU.
+// Pass geometry (N, stages, stride, last) is compile-time, so every element
+// address is one per-thread 32-bit offset plus a constant on a scalar base.
 // Inside a pass each thread keeps R = 16 elements in VGPRs and runs LOGR = 4
 // butterfly stages in registers per "group"; groups are separated by ONE LDS
 // exchange (write, barrier, read).  The first group loads straight from HBM
@@ -34,9 +37,6 @@ struct NttArgs {
   const ModInfo *mods;   // [nmod]
   const u64 *ninv;       // [nmod], N^-1 in Montgomery form
   u32 log_n;
-  u32 s0;                // first global stage of this pass
-  u32 log_stride;        // sub-transform element stride = 2^log_stride
-  u32 last;              // canonicalise output (and scale by N^-1 for INTT)
   // EPI_COMBINE (forward last pass over the ModDown conversion conv [p][L][N],
   // p = 2 ct + b): out[p][i] = (add_mask bit b ? base[p][i] : 0) + (acc[p][i] - conv) P^-1
   const u64 *e_acc;      // [p][e_acc_stride][N]
@@ -68,7 +68,9 @@ struct EpiRow {
 __device__ __forceinline__ u64 ld_at(const u64 *base, u32 idx) {
   return *(const u64 *)((const char *)base + (idx << 3));
 }
-__device__ __forceinline__ void st_at(u64 *base, u32 idx, u64 v) { *(u64 *)((char *)base + (idx << 3)) = v; }
+// the same at a byte offset (per-thread offsets computed once per pass)
+__device__ __forceinline__ u64 ld_b(const u64 *base, u32 off) { return *(const u64 *)((const char *)base + off); }
+__device__ __forceinline__ void st_b(u64 *base, u32 off, u64 v) { *(u64 *)((char *)base + off) = v; }
 
 template <int S>
 __device__ __forceinline__ u32 lds_idx(u32 w, u32 k) {
@@ -84,31 +86,39 @@ constexpr size_t lds_bytes() {
 
 // Group geometry (compile time): group g covers local stages
 // [g*LOGR, g*LOGR + nb); its butterfly bits are k bits [p, p+nb).  A thread
-// holds R = 2^LOGR elements k(r) = hh<<(p+nb+ex) | rx<<(p+nb) | rb<<p | lo_t.
+// holds R = 2^LOGR elements k(r) = hh<<(p+nb+ex) | rx<<(p+nb) | rb<<p | lo_t;
+// k_thr(ts) is the per-thread part, k_reg(r) the compile-time part.
 template <int S, int LOGR, int G>
 struct Grp {
   static constexpr int nb = (S - G * LOGR) < LOGR ? (S - G * LOGR) : LOGR;
   static constexpr int ex = LOGR - nb;
   static constexpr int p = S - G * LOGR - nb;
   static constexpr int NTW = (1 << ex) * ((1 << nb) - 1);  // distinct twiddles per thread
-  __device__ static __forceinline__ u32 k_of(int r, u32 ts) {
-    const u32 rb = r & ((1 << nb) - 1), rx = r >> nb;
-    return ((ts >> p) << (p + nb + ex)) | (rx << (p + nb)) | (rb << p) | (ts & ((1u << p) - 1));
+  __device__ static __forceinline__ u32 k_thr(u32 ts) {
+    return ((ts >> p) << (p + nb + ex)) | (ts & ((1u << p) - 1));
   }
+  static constexpr u32 k_reg(int r) {
+    return ((u32)(r >> nb) << (p + nb)) | ((u32)(r & ((1 << nb) - 1)) << p);
+  }
+  __device__ static __forceinline__ u32 k_of(int r, u32 ts) { return k_thr(ts) | k_reg(r); }
   // slot of (tau, rx, d) in the per-thread twiddle array, d < 2^tau
   __device__ static constexpr int slot(int tau, int rx, int d) { return rx * ((1 << nb) - 1) + (1 << tau) - 1 + d; }
-  __device__ static __forceinline__ void load_tw(u64 (&t)[16], const u64 *tw, u32 s0, u32 hi, u32 ts) {
+  // twiddle of local stage sigma = G*LOGR + tau: index 2^(s0+sigma) + hi 2^sigma + kk,
+  // kk = (hh 2^ex + rx) 2^tau + d.  The thread-dependent part (hi, hh) is one
+  // 32-bit offset per tau; the rest is a compile-time offset on a scalar base.
+  template <int S0>
+  __device__ static __forceinline__ void load_tw(u64 (&t)[16], const u64 *tw, u32 hi, u32 ts) {
     const u32 hh = ts >> p;
 #pragma unroll
-    for (int rx = 0; rx < (1 << ex); ++rx)
+    for (int tau = 0; tau < nb; ++tau) {
+      const int sigma = G * LOGR + tau;
+      const u32 thr = (hi << sigma) + (hh << (ex + tau));
 #pragma unroll
-      for (int tau = 0; tau < nb; ++tau)
+      for (int rx = 0; rx < (1 << ex); ++rx)
 #pragma unroll
-        for (int d = 0; d < (1 << tau); ++d) {
-          const u32 sigma = G * LOGR + tau;
-          const u32 kk = ((((hh << ex) | rx) << tau) | d);
-          t[slot(tau, rx, d)] = ld_at(tw, (1u << (s0 + sigma)) + (hi << sigma) + kk);
-        }
+        for (int d = 0; d < (1 << tau); ++d)
+          t[slot(tau, rx, d)] = ld_at(tw + ((1u << (S0 + sigma)) + ((u32)rx << tau) + (u32)d), thr);
+    }
   }
 };
 
@@ -121,7 +131,18 @@ __device__ __forceinline__ u64 harvey_csub(u64 x, u64 neg_m) {
   return (x & mm) | (d & ~mm);
 }
 
-template <int S, int LOGR, int G, bool INV, bool SP>
+// Forward lazy-range schedule.  NARROW (every modulus): values in [0,4q)
+// between stages, U = csub(X, 2q) at every stage (Harvey).  WIDE (special
+// moduli q < 2^60, i.e. 8q < 2^63, the Montgomery input bound): a stage with
+// input bound B q gives outputs below (B+2) q without any reduction
+// (X' = X + V < (B+1.5) q, Y' = X + 2q - V < (B+2) q), so from an input in
+// [0,4q) the stages run 4 -> 6 -> 8 and then alternate csub(X, 4q) (8 -> 6)
+// with none (6 -> 8): global stages 2, 4, 6, ... reduce, the others do not,
+// and 7 of the 16 stages of N = 2^16 reduce instead of 16.  Pass outputs stay
+// below 8q < 2^63; the last stage canonicalises from [0,8q).
+__host__ __device__ constexpr bool wide_csub(int gs) { return gs >= 2 && (gs & 1) == 0; }
+
+template <int S, int LOGR, int G, int S0, bool INV, bool SP, bool WIDE>
 __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 q2, const ModInfo &mi) {
   using GP = Grp<S, LOGR, G>;
   constexpr int R = 1 << LOGR;
@@ -147,14 +168,17 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
       }
       // 64-bit adds of SGPR constants as single v_lshl_add_u64 (no carry
       // chain through VCC, which costs s_nop wait states): a - b = a + (2q+1) + ~b - 2q
-      u64 nq2 = 0 - q2, q2p1 = q2 + 1;
+      u64 nq2 = 0 - q2, q2p1 = q2 + 1, nq4 = 0 - 2 * q2;
       asm("" : "+s"(nq2));
       asm("" : "+s"(q2p1));
+      asm("" : "+s"(nq4));
+      const int gs = S0 + G * LOGR + tau;  // global stage
+      const bool red = !WIDE || wide_csub(gs);
 #pragma unroll
       for (int i = 0; i < H; ++i) {
         const u64 X = x[lo_idx[i]], Y = x[lo_idx[i] + half];
         if (!INV) {
-          U[i] = harvey_csub(X, nq2);
+          U[i] = !red ? X : harvey_csub(X, WIDE ? nq4 : nq2);
           A[i] = Y;
         } else {
           U[i] = harvey_csub(X + Y, nq2);
@@ -196,10 +220,22 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
   }
 }
 
-template <int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int GI>
+// Compile-time pass geometry.  A pass owns global stages [S0, S0+S) of an
+// N = 2^LOG_N transform; column passes work at element stride 2^LS, row passes
+// on contiguous blocks.  The last pass canonicalises (and scales by N^-1).
+template <int LOG_N, int S, bool COLS, bool INV>
+struct PassGeo {
+  static constexpr bool single = S == LOG_N;
+  static constexpr int S0 = COLS ? 0 : LOG_N - S;
+  static constexpr int LS = COLS ? LOG_N - S : 0;
+  static constexpr bool LAST = single || (COLS == INV);
+};
+
+template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, bool WIDE, int EPI, int GI>
 __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds, const u64 *tw, u64 *data,
-                                           u32 gb, u32 stride, u32 w, u32 ts, u32 hi, const NttArgs &a,
+                                           u32 voff, u32 w, u32 ts, u32 hi, const NttArgs &a,
                                            const ModInfo &mi, u32 mod, const EpiRow &ep) {
+  using PG = PassGeo<LOG_N, S, COLS, INV>;
   constexpr int NG = (S + LOGR - 1) / LOGR;
   constexpr int R = 1 << LOGR;
   constexpr int G = INV ? NG - 1 - GI : GI;
@@ -208,20 +244,30 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
   if constexpr (GI + 1 < NG) {
     constexpr int GN = INV ? NG - 2 - GI : GI + 1;
     u64 tn[16];
-    Grp<S, LOGR, GN>::load_tw(tn, tw, a.s0, hi, ts);  // in flight while this group computes
-    run_group<S, LOGR, G, INV, SP>(x, tc, q2, mi);
+    Grp<S, LOGR, GN>::template load_tw<PG::S0>(tn, tw, hi, ts);  // in flight while this group computes
+    run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
+    const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, GP::k_of(r, ts))] = x[r];
+    for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + (GP::k_reg(r) >> 4)] = x[r];
     __syncthreads();
+    const u32 lr = lds_idx<S>(w, Grp<S, LOGR, GN>::k_thr(ts));
 #pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = lds[lds_idx<S>(w, Grp<S, LOGR, GN>::k_of(r, ts))];
-    group_loop<S, LOGR, W, INV, COLS, SP, EPI, GI + 1>(x, tn, lds, tw, data, gb, stride, w, ts, hi, a, mi, mod, ep);
+    for (int r = 0; r < R; ++r) {
+      const u32 kr = Grp<S, LOGR, GN>::k_reg(r);
+      x[r] = lds[lr + kr + (kr >> 4)];
+    }
+    group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, GI + 1>(x, tn, lds, tw, data, voff, w, ts, hi, a, mi,
+                                                                     mod, ep);
   } else {
-    run_group<S, LOGR, G, INV, SP>(x, tc, q2, mi);
-    if (a.last) {
-      if (!INV) {
+    run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
+    if constexpr (PG::LAST) {
+      if constexpr (!INV) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = harvey_csub(harvey_csub(x[r], 0 - q2), 0 - q);
+        for (int r = 0; r < R; ++r) {
+          u64 v = x[r];
+          if (WIDE) v = harvey_csub(v, 0 - 2 * q2);
+          x[r] = harvey_csub(harvey_csub(v, 0 - q2), 0 - q);
+        }
       } else {
         const u64 sc = a.ninv[mod];
 #pragma unroll
@@ -231,39 +277,90 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     if constexpr (!COLS && G != 0) {
       // row pass ending in a group whose lanes each own contiguous words:
       // re-layout through LDS so the HBM store is coalesced (group-0 layout)
+      const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
 #pragma unroll
-      for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, GP::k_of(r, ts))] = x[r];
+      for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + (GP::k_reg(r) >> 4)] = x[r];
       __syncthreads();
+      using G0 = Grp<S, LOGR, 0>;
+      const u32 lr = lds_idx<S>(w, G0::k_thr(ts));
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const u32 k = Grp<S, LOGR, 0>::k_of(r, ts);
-        const u64 v = lds[lds_idx<S>(w, k)];
+        const u32 kr = G0::k_reg(r);
+        const u64 v = lds[lr + kr + (kr >> 4)];
         if constexpr (EPI == EPI_COMBINE) {
           // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM
-          const u32 o = gb + k;
-          u64 ks = harvey_csub(mont_mul<SP>(sub_mod(ld_at(ep.acc, o), v, q), ep.pinv, mi), 0 - q);
-          if (ep.add) ks = add_mod(ks, ld_at(ep.base, o), q);
-          st_at(ep.out, o, ks);
+          u64 ks = harvey_csub(mont_mul<SP>(sub_mod(ld_b(ep.acc + kr, voff), v, q), ep.pinv, mi), 0 - q);
+          if (ep.add) ks = add_mod(ks, ld_b(ep.base + kr, voff), q);
+          st_b(ep.out + kr, voff, ks);
         } else {
-          st_at(data, gb + k, v);
+          st_b(data + kr, voff, v);
         }
       }
     } else {
       static_assert(EPI == EPI_NONE, "epilogues run in the re-laid-out row store");
+      // column pass (or single pass ending in group 0): element k of this
+      // thread sits at voff + k_reg(r) << LS -- a compile-time offset on the
+      // scalar base, so the address costs no VALU
 #pragma unroll
-      for (int r = 0; r < R; ++r) st_at(data, gb + (GP::k_of(r, ts) << a.log_stride), x[r]);
+      for (int r = 0; r < R; ++r) st_b(data + ((size_t)GP::k_reg(r) << PG::LS), voff, x[r]);
     }
   }
 }
 
-template <int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI>
+template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, bool WIDE, int EPI>
+__device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data, const u64 *tw, const ModInfo &mi,
+                                          u32 mod, u32 w, u32 ts, u32 hi, u32 gb, const EpiRow &ep) {
+  using PG = PassGeo<LOG_N, S, COLS, INV>;
+  constexpr int R = 1 << LOGR;
+  constexpr int NG = (S + LOGR - 1) / LOGR;
+  constexpr int G0 = INV ? NG - 1 : 0;
+  u64 tc[16];
+  Grp<S, LOGR, G0>::template load_tw<PG::S0>(tc, tw, hi, ts);
+  u64 x[R];
+  u32 voff;  // byte offset of this thread's element k_thr of the first (HBM) group layout
+  if constexpr (!COLS && G0 != 0) {
+    // row pass starting in a per-lane-contiguous group: coalesced load in the
+    // group-0 layout, then one LDS re-layout
+    using GZ = Grp<S, LOGR, 0>;
+    voff = (gb + GZ::k_thr(ts)) << 3;
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = ld_b(data + GZ::k_reg(r), voff);
+    const u32 lw = lds_idx<S>(w, GZ::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[lw + GZ::k_reg(r) + (GZ::k_reg(r) >> 4)] = x[r];
+    __syncthreads();
+    using GF = Grp<S, LOGR, G0>;
+    const u32 lr = lds_idx<S>(w, GF::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u32 kr = GF::k_reg(r);
+      x[r] = lds[lr + kr + (kr >> 4)];
+    }
+  } else {
+    using GF = Grp<S, LOGR, G0>;
+    voff = (gb + (GF::k_thr(ts) << PG::LS)) << 3;
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = ld_b(data + ((size_t)GF::k_reg(r) << PG::LS), voff);
+  }
+  // the final store uses the group-0 layout for row passes and the last
+  // group's layout for column passes; recompute the offset for the latter
+  if constexpr (COLS) {
+    constexpr int GL = INV ? 0 : NG - 1;
+    voff = (gb + (Grp<S, LOGR, GL>::k_thr(ts) << PG::LS)) << 3;
+  } else {
+    voff = (gb + Grp<S, LOGR, 0>::k_thr(ts)) << 3;
+  }
+  group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, 0>(x, tc, lds, tw, data, voff, w, ts, hi, a, mi, mod, ep);
+}
+
+template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI>
 __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE, "ntt_pass epilogues");
   static_assert(EPI == EPI_NONE || (!INV && !COLS), "epilogues follow a forward row pass");
-  constexpr int R = 1 << LOGR;
+  using PG = PassGeo<LOG_N, S, COLS, INV>;
+  static_assert(EPI == EPI_NONE || PG::LAST, "epilogues run in the last pass");
   constexpr int T = 1 << (S - LOGR);
-  constexpr int NG = (S + LOGR - 1) / LOGR;
-  static_assert(R == 16, "register tile is 16 words");
+  static_assert(LOGR == 4, "register tile is 16 words");
   extern __shared__ u64 lds[];
 
   // (poly, limb) come from gridDim.y / gridDim.z, so every per-workgroup
@@ -273,115 +370,97 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   const u32 poly = blockIdx.y, act = blockIdx.z;
   const u32 limb = limbmap_limb(a.map, act);
   const u32 mod = a.map.mod_offset + limb;
-  u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << a.log_n);
+  u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
   const ModInfo mi = a.mods[mod];
-  const u64 *tw = a.tw + ((size_t)mod << a.log_n);
-  const u32 stride = 1u << a.log_stride;
+  const u64 *tw = a.tw + ((size_t)mod << LOG_N);
+  constexpr u32 stride = 1u << PG::LS;
 
   // column passes put the W sub-transforms (adjacent columns) on adjacent
   // lanes: every wave access is four 128 B row segments
   u32 w, ts;
   if (COLS) { w = tid % W; ts = tid / W; } else { ts = tid % T; w = tid / T; }
   const u32 u = blockIdx.x * W + w;
-  const u32 hi = u >> a.log_stride;
-  const u32 gb = (hi << (S + a.log_stride)) + (u & (stride - 1));
+  const u32 hi = u >> PG::LS;
+  const u32 gb = (hi << (S + PG::LS)) + (u & (stride - 1));
 
-  constexpr int G0 = INV ? NG - 1 : 0;
-  u64 tc[16];
-  Grp<S, LOGR, G0>::load_tw(tc, tw, a.s0, hi, ts);
-  u64 x[R];
-  if constexpr (!COLS && G0 != 0) {
-    // row pass starting in a per-lane-contiguous group: coalesced load in the
-    // group-0 layout, then one LDS re-layout
-#pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = ld_at(data, gb + Grp<S, LOGR, 0>::k_of(r, ts));
-#pragma unroll
-    for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, Grp<S, LOGR, 0>::k_of(r, ts))] = x[r];
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = lds[lds_idx<S>(w, Grp<S, LOGR, G0>::k_of(r, ts))];
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = ld_at(data, gb + (Grp<S, LOGR, G0>::k_of(r, ts) << a.log_stride));
-  }
   EpiRow ep{};
   if constexpr (EPI == EPI_COMBINE) {
-    ep.acc = a.e_acc + (((size_t)poly * a.e_acc_stride + limb) << a.log_n);
-    ep.base = a.e_base + (((size_t)poly * a.map.poly_stride + limb) << a.log_n);
-    ep.out = a.e_out + (((size_t)poly * a.map.poly_stride + limb) << a.log_n);
+    ep.acc = a.e_acc + (((size_t)poly * a.e_acc_stride + limb) << LOG_N);
+    ep.base = a.e_base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
+    ep.out = a.e_out + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
     ep.pinv = a.e_pinv[limb];
     ep.add = (a.e_add_mask >> (poly & 1)) & 1;
   }
-  group_loop<S, LOGR, W, INV, COLS, SP, EPI, 0>(x, tc, lds, tw, data, gb, stride, w, ts, hi, a, mi, mod, ep);
+  if constexpr (SP && !INV) {
+    // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)
+    if (mi.q < (1ull << 60)) {
+      pass_body<LOG_N, S, LOGR, W, INV, COLS, SP, true, EPI>(a, lds, data, tw, mi, mod, w, ts, hi, gb, ep);
+      return;
+    }
+  }
+  pass_body<LOG_N, S, LOGR, W, INV, COLS, SP, false, EPI>(a, lds, data, tw, mi, mod, w, ts, hi, gb, ep);
 }
 
-template <int S, int W, bool COLS, bool INV, bool SP, int EPI>
+template <int LOG_N, int S, int W, bool COLS, bool INV, bool SP, int EPI>
 int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   constexpr int LOGR = 4;
   constexpr int NT = W << (S - LOGR);
   constexpr size_t lds = lds_bytes<S, W>();
-  const u32 subs = 1u << (a.log_n - S);
+  constexpr u32 subs = 1u << (LOG_N - S);
   // dispatch order: row blocks, then polys, then limbs -- the resident
   // workgroups share one modulus, so its twiddle table stays in L2
   dim3 grid(subs / W, n_jobs / a.map.cnt, a.map.cnt);
-  auto k = ntt_pass<S, LOGR, W, INV, COLS, SP, EPI>;
+  auto k = ntt_pass<LOG_N, S, LOGR, W, INV, COLS, SP, EPI>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);
   return fhe_check(c, hipGetLastError(), "ntt_pass launch");
 }
 
-template <int S, int W, bool COLS, int EPI = EPI_NONE>
+template <int LOG_N, int S, int W, bool COLS, int EPI = EPI_NONE>
 int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
   if constexpr (EPI != EPI_NONE) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
-    return c->special ? launch_one<S, W, COLS, false, true, EPI>(c, a, n_jobs)
-                      : launch_one<S, W, COLS, false, false, EPI>(c, a, n_jobs);
+    return c->special ? launch_one<LOG_N, S, W, COLS, false, true, EPI>(c, a, n_jobs)
+                      : launch_one<LOG_N, S, W, COLS, false, false, EPI>(c, a, n_jobs);
   } else {
     if (c->special)
-      return inv ? launch_one<S, W, COLS, true, true, EPI>(c, a, n_jobs)
-                 : launch_one<S, W, COLS, false, true, EPI>(c, a, n_jobs);
-    return inv ? launch_one<S, W, COLS, true, false, EPI>(c, a, n_jobs)
-               : launch_one<S, W, COLS, false, false, EPI>(c, a, n_jobs);
+      return inv ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
+                 : launch_one<LOG_N, S, W, COLS, false, true, EPI>(c, a, n_jobs);
+    return inv ? launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs)
+               : launch_one<LOG_N, S, W, COLS, false, false, EPI>(c, a, n_jobs);
   }
 }
 
 // one pass over a whole residue (N <= 2^14)
 template <int EPI = EPI_NONE>
-int single_pass(fhe_ctx *c, NttArgs a, bool inv, u32 n_jobs) {
-  a.s0 = 0;
-  a.log_stride = 0;
-  a.last = 1;
+int single_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
   switch (a.log_n) {
-    case 10: return launch_pass<10, 1, false, EPI>(c, a, inv, n_jobs);
-    case 11: return launch_pass<11, 1, false, EPI>(c, a, inv, n_jobs);
-    case 12: return launch_pass<12, 1, false, EPI>(c, a, inv, n_jobs);
-    case 13: return launch_pass<13, 1, false, EPI>(c, a, inv, n_jobs);
-    case 14: return launch_pass<14, 1, false, EPI>(c, a, inv, n_jobs);
+    case 10: return launch_pass<10, 10, 1, false, EPI>(c, a, inv, n_jobs);
+    case 11: return launch_pass<11, 11, 1, false, EPI>(c, a, inv, n_jobs);
+    case 12: return launch_pass<12, 12, 1, false, EPI>(c, a, inv, n_jobs);
+    case 13: return launch_pass<13, 13, 1, false, EPI>(c, a, inv, n_jobs);
+    case 14: return launch_pass<14, 14, 1, false, EPI>(c, a, inv, n_jobs);
   }
   return fhe_fail(c, FHE_ERR_UNSUPPORTED, "single_pass: log_n");
 }
 
 // column pass: stages [0, S1), stride N >> S1
-int col_pass(fhe_ctx *c, NttArgs a, bool inv, u32 n_jobs, bool last) {
-  a.s0 = 0;
-  a.last = last;
+int col_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
   switch (a.log_n) {
-    case 15: a.log_stride = 15 - 7; return launch_pass<7, 32, true>(c, a, inv, n_jobs);
-    case 16: a.log_stride = 16 - 8; return launch_pass<8, 16, true>(c, a, inv, n_jobs);
-    case 17: a.log_stride = 17 - 8; return launch_pass<8, 16, true>(c, a, inv, n_jobs);
+    case 15: return launch_pass<15, 7, 32, true>(c, a, inv, n_jobs);
+    case 16: return launch_pass<16, 8, 16, true>(c, a, inv, n_jobs);
+    case 17: return launch_pass<17, 8, 16, true>(c, a, inv, n_jobs);
   }
   return fhe_fail(c, FHE_ERR_UNSUPPORTED, "col_pass: log_n");
 }
 
 // row pass: stages [S1, logN), contiguous blocks
 template <int EPI = EPI_NONE>
-int row_pass(fhe_ctx *c, NttArgs a, bool inv, u32 n_jobs, bool last) {
-  a.log_stride = 0;
-  a.last = last;
+int row_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
   switch (a.log_n) {
-    case 15: a.s0 = 7; return launch_pass<8, 16, false, EPI>(c, a, inv, n_jobs);
-    case 16: a.s0 = 8; return launch_pass<8, 16, false, EPI>(c, a, inv, n_jobs);
-    case 17: a.s0 = 8; return launch_pass<9, 8, false, EPI>(c, a, inv, n_jobs);
+    case 15: return launch_pass<15, 8, 16, false, EPI>(c, a, inv, n_jobs);
+    case 16: return launch_pass<16, 8, 16, false, EPI>(c, a, inv, n_jobs);
+    case 17: return launch_pass<17, 9, 8, false, EPI>(c, a, inv, n_jobs);
   }
   return fhe_fail(c, FHE_ERR_UNSUPPORTED, "row_pass: log_n");
 }
@@ -412,13 +491,13 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse) {
   if (c->log_n <= 14) return single_pass(c, a, inverse, n_jobs);
   int rc;
   if (!inverse) {
-    rc = col_pass(c, a, false, n_jobs, false);
+    rc = col_pass(c, a, false, n_jobs);
     if (rc) return rc;
-    return row_pass(c, a, false, n_jobs, true);
+    return row_pass(c, a, false, n_jobs);
   }
-  rc = row_pass(c, a, true, n_jobs, false);
+  rc = row_pass(c, a, true, n_jobs);
   if (rc) return rc;
-  return col_pass(c, a, true, n_jobs, true);
+  return col_pass(c, a, true, n_jobs);
 }
 
 // Forward NTT of the ModDown conversion conv (all L limbs of 2n polys) with
@@ -449,8 +528,8 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
     if (c->log_n <= 14) {
       rc = single_pass<EPI_COMBINE>(c, a, false, n_jobs);
     } else {
-      if ((rc = col_pass(c, a, false, n_jobs, false))) return rc;
-      rc = row_pass<EPI_COMBINE>(c, a, false, n_jobs, true);
+      if ((rc = col_pass(c, a, false, n_jobs))) return rc;
+      rc = row_pass<EPI_COMBINE>(c, a, false, n_jobs);
     }
     if (rc) return rc;
   }
