@@ -91,13 +91,19 @@ HD u64 mont_reduce(U128 T, const ModInfo &m) {
 }
 
 // Special-modulus Montgomery product by word-serial CIOS: a < 2^63, b < q < 2^61,
-// q = q_hi * 2^32 + 1.  Six v_mad_u64_u32 and no 128-bit carry chains: the
+// q = q_hi * 2^32 + 1.  Six v_mad_u64_u32, two v_not and no 64-bit add: the
 // bounds a_hi < 2^31 and b_hi < 2^29 keep every partial sum below 2^64.
 // Returns a*b*2^-64 mod q in [0, 1.5q).
-// Each "+ (p0 != 0)" carry of a Montgomery round is folded into the multiply-add
-// that produces the word: P' = a0 b0 + (2^32 - 1) has P'.hi = P.hi + (P.lo != 0)
-// and ~P'.lo = -P.lo mod 2^32.  OPAQUE keeps the compiler from rewriting
-// ~P'.lo back into a (slow) v_mul_lo_u32 of the operands.
+//  * round 1 uses m0 = -P.lo mod 2^32; its "+ (P.lo != 0)" carry is folded into
+//    the multiply-add that produces the word: P' = a0 b0 + (2^32 - 1) has
+//    P'.hi = P.hi + (P.lo != 0) and ~P'.lo = m0;
+//  * round 2 uses the integer multiplier m1 = ~X.lo + 1 in [1, 2^32] (still
+//    = -X.lo mod 2^32, so X + m1 q is divisible by 2^32 and the quotient is
+//    X.hi + 1 + ~X.lo q_hi + q_hi): its constant 1 + q_hi rides in the HIGH
+//    word of round 1's 64-bit addend pair {P'.hi, 1 + q_hi}, which otherwise
+//    holds a zero register -- the carry costs no instruction at all.
+// OPAQUE keeps the compiler from rewriting ~P'.lo back into a (slow)
+// v_mul_lo_u32 of the operands and from re-associating the mad chains.
 #if defined(__HIP_DEVICE_COMPILE__)
 #define OPAQUE(x) asm("" : "+v"(x))
 #else
@@ -105,11 +111,12 @@ HD u64 mont_reduce(U128 T, const ModInfo &m) {
 #endif
 HD u64 mont_mul_sp(u64 a, u64 b, u32 q_hi) {
   const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+  const u64 csh = (u64)(q_hi + 1) << 32;
   u64 P = (u64)a0 * b0 + 0xFFFFFFFFull;
   OPAQUE(P);
-  u64 V = (u64)(~(u32)P) * q_hi + ((u64)a1 * b0 + (P >> 32));  // (a b0 + m q) / 2^32
+  u64 V = (u64)(~(u32)P) * q_hi + ((u64)a1 * b0 + ((P >> 32) | csh));  // (a b0 + m0 q) / 2^32 + (1 + q_hi) 2^32
   OPAQUE(V);
-  u64 X0 = (u64)a0 * b1 + V + 0xFFFFFFFFull;                         // + a0 b1, carry folded
+  u64 X0 = (u64)a0 * b1 + V;
   OPAQUE(X0);
   return (u64)(~(u32)X0) * q_hi + ((u64)a1 * b1 + (X0 >> 32));
 }
@@ -118,6 +125,7 @@ HD u64 mont_mul_sp(u64 a, u64 b, u32 q_hi) {
 // multiply chains of different products interleave in the instruction stream.
 template <int M>
 HD void mont_mul_sp_vec(u64 (&r)[M], const u64 (&a)[M], const u64 (&b)[M], u32 q_hi) {
+  const u64 csh = (u64)(q_hi + 1) << 32;
   u64 t[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
@@ -126,12 +134,12 @@ HD void mont_mul_sp_vec(u64 (&r)[M], const u64 (&a)[M], const u64 (&b)[M], u32 q
   }
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    t[i] = (u64)(~(u32)t[i]) * q_hi + ((u64)(u32)(a[i] >> 32) * (u32)b[i] + (t[i] >> 32));  // V
+    t[i] = (u64)(~(u32)t[i]) * q_hi + ((u64)(u32)(a[i] >> 32) * (u32)b[i] + ((t[i] >> 32) | csh));  // V
     OPAQUE(t[i]);  // keep the mad chain as written (no re-association into extra adds)
   }
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    t[i] = (u64)(u32)a[i] * (u32)(b[i] >> 32) + t[i] + 0xFFFFFFFFull;  // X0'
+    t[i] = (u64)(u32)a[i] * (u32)(b[i] >> 32) + t[i];  // X
     OPAQUE(t[i]);
   }
 #pragma unroll
