@@ -83,7 +83,9 @@ _lib = None
 
 
 def library_path() -> str:
-    return os.path.join(HERE, "lib", "libherdsman_fhe.so")
+    # HERD_FHE_LIB selects another in-tree build of the same library (A/B
+    # experiments on the GPU box); it is still the HIP backend, never a fallback
+    return os.environ.get("HERD_FHE_LIB") or os.path.join(HERE, "lib", "libherdsman_fhe.so")
 
 
 def load_library():
