@@ -344,7 +344,11 @@ int fhe_dev_free(fhe_ctx *c, void *ptr) {
 }
 int fhe_memcpy_h2d(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
   if (!c) return FHE_ERR_INVALID;
-  return fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream), "h2d");
+  int rc = fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream), "h2d");
+  if (rc) return rc;
+  // the host buffer may be reused as soon as this returns (callers stage
+  // successive inputs through one pageable buffer)
+  return fhe_check(c, hipStreamSynchronize(c->stream), "h2d sync");
 }
 int fhe_memcpy_d2h(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
   if (!c) return FHE_ERR_INVALID;

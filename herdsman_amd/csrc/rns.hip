@@ -78,9 +78,10 @@ __device__ __forceinline__ void conv_stage(ConvLds<NS> &sh, const ConvTab &t, co
   }
 }
 // y_m = sum_i v_i h[i][m] for every target m, streamed to out[slot(m) * N]
-// (slot = the target's modulus id when by_mod, else m)
-template <int NS, bool SP>
-__device__ __forceinline__ void conv_store(const ConvLds<NS> &sh, const u64 (&v)[NS], u32 ns, u32 nd, u64 *out,
+// (slot = the target's modulus id when by_mod, else m), for the CPT
+// coefficients of this thread (at stride EW_BLOCK)
+template <int NS, bool SP, int CPT>
+__device__ __forceinline__ void conv_store(const ConvLds<NS> &sh, const u64 (&v)[CPT][NS], u32 ns, u32 nd, u64 *out,
                                            size_t N, bool by_mod, u32 mod_base) {
 #pragma unroll 1
   for (u32 m = 0; m < nd; ++m) {
@@ -88,7 +89,30 @@ __device__ __forceinline__ void conv_store(const ConvLds<NS> &sh, const u64 (&v)
     mi.q = sh.q[m];
     mi.q_hi = (u32)sh.aux[m];
     mi.qinv_neg = sh.aux[m];
-    st_nt(out + (by_mod ? sh.dm[m] - mod_base : m) * N, dot_mont<NS, SP>(v, sh.h + m, nd, ns, mi));
+    u64 *o = out + (by_mod ? sh.dm[m] - mod_base : m) * N;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) st_nt(o + c * EW_BLOCK, dot_mont<NS, SP>(v[c], sh.h + m, nd, ns, mi));
+  }
+}
+
+// Coefficients per thread of the conversion kernels: the per-workgroup table
+// staging (a chain of dependent loads and a barrier) is amortised over
+// CPT * EW_BLOCK coefficients, each thread has CPT * ns source loads in
+// flight, and they are issued before the staging so their latency overlaps it.
+constexpr int CONV_CPT = 2;
+
+// v_i = [x_i (S/s_i)^-1]_{s_i} for the CPT coefficients (source i uses
+// modulus src_mod[i], or mod0 + i when src_mod is null)
+template <int NS, bool SP>
+__device__ __forceinline__ void conv_scale(u64 (&v)[CONV_CPT][NS], const u64 (&x)[CONV_CPT][NS], const ConvTab &t,
+                                           const ModInfo *mods, const u32 *src_mod, u32 mod0) {
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const bool on = i < (int)t.ns;
+    const ModInfo ms = mods[src_mod ? src_mod[on ? i : 0] : mod0 + (on ? i : 0)];
+    const u64 hv = t.hinv[on ? i : 0];
+#pragma unroll
+    for (int c = 0; c < CONV_CPT; ++c) v[c][i] = on ? csub(mont_mul<SP>(x[c][i], hv, ms), ms.q) : 0;
   }
 }
 
@@ -98,22 +122,20 @@ __global__ void __launch_bounds__(EW_BLOCK) conv_kernel(const u64 *__restrict__ 
                                                         u64 *__restrict__ dst, u32 dst_stride, ConvTab t,
                                                         const ModInfo *mods, u32 log_n) {
   __shared__ ConvLds<NS> sh;
-  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 k = blockIdx.x * (EW_BLOCK * CONV_CPT) + threadIdx.x;
   const u32 p = blockIdx.y;
   const size_t N = (size_t)1 << log_n;
-  conv_stage<NS, SP>(sh, t, mods);
   const u64 *s = src + (size_t)p * src_stride * N + k;
-  u64 v[NS];
+  u64 x[CONV_CPT][NS];
 #pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    v[i] = 0;
-    if (i < (int)t.ns) {
-      const ModInfo ms = mods[t.src_mod[i]];
-      v[i] = csub(mont_mul<SP>(ld_nt(s + i * N), t.hinv[i], ms), ms.q);
-    }
-  }
+  for (int i = 0; i < NS; ++i)
+#pragma unroll
+    for (int c = 0; c < CONV_CPT; ++c) x[c][i] = i < (int)t.ns ? ld_nt(s + i * N + c * EW_BLOCK) : 0;
+  conv_stage<NS, SP>(sh, t, mods);
+  u64 v[CONV_CPT][NS];
+  conv_scale<NS, SP>(v, x, t, mods, t.src_mod, 0);
   __syncthreads();
-  conv_store<NS, SP>(sh, v, t.ns, t.nd, dst + (size_t)p * dst_stride * N + k, N, false, 0);
+  conv_store<NS, SP, CONV_CPT>(sh, v, t.ns, t.nd, dst + (size_t)p * dst_stride * N + k, N, false, 0);
 }
 
 // ModUp (keyswitch_one, oracle): every limb of Q u P outside digit j is the
@@ -122,31 +144,29 @@ __global__ void __launch_bounds__(EW_BLOCK) conv_kernel(const u64 *__restrict__ 
 // automorph).  Outputs are written times R (Montgomery form) so the KS inner
 // product needs a single reduction.  The conversion table of the digit and the
 // destination moduli are staged in LDS once per workgroup, so the per-target
-// loop issues no dependent global/scalar loads.
+// loop issues no dependent global/scalar loads (CONV_CPT coefficients per thread).
 template <int NS, bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__ dc, u32 dc_stride,
                                                          u64 *__restrict__ ext, const ConvTab *tabs,
                                                          const ModInfo *mods, u32 QP, u32 alpha, u32 ndig,
                                                          u32 log_n) {
   __shared__ ConvLds<NS> sh;
-  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 k = blockIdx.x * (EW_BLOCK * CONV_CPT) + threadIdx.x;
   const u32 ct = blockIdx.y / ndig, j = blockIdx.y % ndig;
   const size_t N = (size_t)1 << log_n;
   const u32 lo = j * alpha;
   const ConvTab t = tabs[j];
-  conv_stage<NS, SP>(sh, t, mods);
   const u64 *s = dc + ((size_t)ct * dc_stride + lo) * N + k;
-  u64 v[NS];
+  u64 x[CONV_CPT][NS];
 #pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    v[i] = 0;
-    if (i < (int)t.ns) {
-      const ModInfo ms = mods[lo + i];
-      v[i] = csub(mont_mul<SP>(ld_nt(s + i * N), t.hinv[i], ms), ms.q);
-    }
-  }
+  for (int i = 0; i < NS; ++i)
+#pragma unroll
+    for (int c = 0; c < CONV_CPT; ++c) x[c][i] = i < (int)t.ns ? ld_nt(s + i * N + c * EW_BLOCK) : 0;
+  conv_stage<NS, SP>(sh, t, mods);
+  u64 v[CONV_CPT][NS];
+  conv_scale<NS, SP>(v, x, t, mods, nullptr, lo);
   __syncthreads();
-  conv_store<NS, SP>(sh, v, t.ns, t.nd, ext + ((size_t)(ct * ndig + j) * QP) * N + k, N, true, 0);
+  conv_store<NS, SP, CONV_CPT>(sh, v, t.ns, t.nd, ext + ((size_t)(ct * ndig + j) * QP) * N + k, N, true, 0);
 }
 
 // KS preparation for an input d (fhe_keyswitch, BFV): dc = d and the own-digit
@@ -192,13 +212,22 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restric
       k0[j] = j < (int)ndig ? kp[(size_t)(2 * j) * QP * N] : 0;
       k1[j] = j < (int)ndig ? kp[(size_t)(2 * j + 1) * QP * N] : 0;
     }
+    // software pipeline over the batch: the next ciphertext's digit words are
+    // in flight while this one's products are formed
+    u64 x[MAXD];
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j) x[j] = (j < (int)ndig && n_ct) ? ld_nt(e + (size_t)j * QP * N) : 0;
 #pragma unroll 1
     for (u32 ct = 0; ct < n_ct; ++ct) {
-      u64 x[MAXD];
+      u64 xn[MAXD];
+      const bool more = ct + 1 < n_ct;
 #pragma unroll
-      for (int j = 0; j < MAXD; ++j) x[j] = j < (int)ndig ? ld_nt(e + ct * ext_ct + (size_t)j * QP * N) : 0;
+      for (int j = 0; j < MAXD; ++j)
+        xn[j] = (j < (int)ndig && more) ? ld_nt(e + (ct + 1) * ext_ct + (size_t)j * QP * N) : 0;
       st_nt(o + ct * acc_ct, dot_mont<MAXD, SP>(x, k0, 1, ndig, m));
       st_nt(o + ct * acc_ct + (size_t)QP * N, dot_mont<MAXD, SP>(x, k1, 1, ndig, m));
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) x[j] = xn[j];
     }
   } else {
     // many digits (> 16): stream the key words with the digits, 4 at a time
@@ -457,7 +486,7 @@ int ew_impl(fhe_ctx *c, EwOp op, const u64 *a, const u64 *b, u64 *out, u32 jobs,
 
 template <bool SP>
 int conv_impl(fhe_ctx *c, const ConvTab &t, const u64 *src, u32 ss, u64 *dst, u32 ds, u32 n) {
-  dim3 grid(c->n / EW_BLOCK, n);
+  dim3 grid(c->n / (EW_BLOCK * CONV_CPT), n);
   if (t.ns <= 4) hipLaunchKernelGGL((conv_kernel<4, SP>), grid, dim3(EW_BLOCK), 0, c->stream, src, ss, dst, ds, t, c->d_mods, c->log_n);
   else if (t.ns <= 8) hipLaunchKernelGGL((conv_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, src, ss, dst, ds, t, c->d_mods, c->log_n);
   else if (t.ns <= 16) hipLaunchKernelGGL((conv_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, src, ss, dst, ds, t, c->d_mods, c->log_n);
@@ -467,7 +496,7 @@ int conv_impl(fhe_ctx *c, const ConvTab &t, const u64 *src, u32 ss, u64 *dst, u3
 
 template <bool SP>
 int modup_impl(fhe_ctx *c, const u64 *dc, u32 dcs, u64 *ext, u32 n, u32 ndig) {
-  dim3 grid(c->n / EW_BLOCK, n * ndig);
+  dim3 grid(c->n / (EW_BLOCK * CONV_CPT), n * ndig);
   const u32 QP = c->L + c->K;
   if (c->alpha <= 4)
     hipLaunchKernelGGL((modup_kernel<4, SP>), grid, dim3(EW_BLOCK), 0, c->stream, dc, dcs, ext, c->d_modup, c->d_mods, QP, c->alpha, ndig, c->log_n);

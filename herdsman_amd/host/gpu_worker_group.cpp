@@ -404,8 +404,8 @@ void GpuWorkerGroup::device_loop(Device &dev) {
     }
     complete(job.handle, st);
   }
+  dev.keys.clear();  // key buffers are freed through their context: before it goes
   for (auto &kv : dev.ctx) fhe_ctx_destroy(kv.second.ctx);
-  dev.keys.clear();
 }
 
 }  // namespace herdsman_gpu

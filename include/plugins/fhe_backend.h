@@ -83,6 +83,7 @@ int fhe_reserve(fhe_ctx *ctx, uint32_t max_batch);
 /* ---- device memory helpers (for callers without their own allocator) -- */
 int fhe_dev_alloc(fhe_ctx *ctx, size_t bytes, void **out);
 int fhe_dev_free(fhe_ctx *ctx, void *ptr);
+/* h2d returns once the host buffer may be reused; d2h returns once the data has arrived */
 int fhe_memcpy_h2d(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
 int fhe_memcpy_d2h(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
 

@@ -73,6 +73,27 @@ def test_ntt_vs_oracle(hb, log_n, L, polys):
     assert np.array_equal(hb.to_host(d), o.ntt_inv(x))
 
 
+@pytest.mark.parametrize("log_n,L,K", [(12, 2, 1), (15, 2, 1), (16, 3, 2)])
+def test_ntt_fwd_lazy_inputs(hb, log_n, L, K):
+    """The forward NTT accepts lazy inputs in [0, 4q) (the oracle's Harvey bound)
+    on both lazy schedules: the wide one (60-bit Q primes, reductions skipped
+    down to 7 of 16 stages) and the narrow one (61-bit P primes)."""
+    o, c = pair(hb, SCHEME_CKKS, log_n, L, K=K, dnum=1)
+    n, nm = 1 << log_n, L + K
+    x = o.uniform((2, nm, n), seed=log_n * 7 + nm)
+    q = np.asarray(o.moduli[:nm], dtype=np.uint64)[None, :, None]
+    lazy = x + (np.arange(2 * nm * n, dtype=np.uint64).reshape(2, nm, n) % np.uint64(4)) * q
+    lazy[0, :, :8] = 4 * q[0] - np.uint64(1)  # the top of the range
+    assert int(lazy.max()) < 4 * int(max(o.moduli[:nm]))
+    want = o.ntt_fwd(x)
+    d = hb.to_device(lazy)
+    c.ntt_fwd(d)
+    want_top = o.ntt_fwd(np.where(np.arange(n)[None, None, :] < 8, (4 * q - np.uint64(1)) % q, x)[:1])
+    got = hb.to_host(d)
+    assert np.array_equal(got[1:], want[1:])
+    assert np.array_equal(got[:1], want_top)
+
+
 def test_ntt_c2_config(hb):
     """BASELINE.json configs[1]: forward+inverse NTT, N=2^14, 4 limbs, bit-exact vs CPU."""
     o, c = pair(hb, SCHEME_CKKS, 14, 4)
