@@ -45,17 +45,30 @@ struct NttArgs {
   const u64 *e_pinv;     // [L] P^-1 R mod q_i
   u32 e_acc_stride;
   u32 e_add_mask;
+  // PRO_TENSOR (first pass of the inverse NTT of d2 in CKKS mul+relin, poly =
+  // ciphertext): the pass reads the operands a, b [ct][2][L][N] instead of d2,
+  // writes the relinearisation base out[ct][0] = a0 b0, out[ct][1] = a0 b1 + a1 b0
+  // and the own-digit ext slot d2 R, and transforms d2 = a1 b1 (the tensor
+  // product fused here: d2 never makes an HBM round trip before the INTT)
+  const u64 *t_a, *t_b;
+  u64 *t_out;            // may alias t_a / t_b (element-wise)
+  u64 *t_ext;            // [ct][ndig][QP][N]
+  u32 t_L, t_QP, t_alpha, t_ndig;
 };
 
-enum { EPI_NONE = 0, EPI_COMBINE = 1 };
+// EPI_COMBINE: epilogue of a forward last pass; PRO_TENSOR: prologue of an
+// inverse first (row) pass
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2 };
 
-// per-workgroup epilogue operands (resolved once per limb)
+// per-workgroup epilogue / prologue operands (resolved once per limb)
 struct EpiRow {
   const u64 *acc;
   const u64 *base;
   u64 *out;
   u64 pinv;
   bool add;
+  const u64 *a0, *a1, *b0, *b1;  // PRO_TENSOR
+  u64 *o0, *o1, *ext;
 };
 
 // LDS slot of element k of sub-transform w: one pad word per 16 words and per
@@ -297,7 +310,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
         }
       }
     } else {
-      static_assert(EPI == EPI_NONE, "epilogues run in the re-laid-out row store");
+      static_assert(EPI != EPI_COMBINE, "epilogues run in the re-laid-out row store");
       // column pass (or single pass ending in group 0): element k of this
       // thread sits at voff + k_reg(r) << LS -- a compile-time offset on the
       // scalar base, so the address costs no VALU
@@ -323,8 +336,25 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
     // group-0 layout, then one LDS re-layout
     using GZ = Grp<S, LOGR, 0>;
     voff = (gb + GZ::k_thr(ts)) << 3;
+    if constexpr (EPI == PRO_TENSOR) {
+      // the CKKS tensor formulas, element-wise at the coalesced positions
 #pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = ld_b(data + GZ::k_reg(r), voff);
+      for (int r = 0; r < R; ++r) {
+        const u32 kr = GZ::k_reg(r);
+        const u64 a0 = ld_b(ep.a0 + kr, voff), a1 = ld_b(ep.a1 + kr, voff);
+        const u64 b0 = ld_b(ep.b0 + kr, voff), b1 = ld_b(ep.b1 + kr, voff);
+        st_b(ep.o0 + kr, voff, mul_mod<SP>(a0, b0, mi));
+        U128 s = mul128(a0, b1);
+        mac128(s, a1, b0);
+        st_b(ep.o1 + kr, voff, reduce128<SP>(s, mi));
+        const u64 t = mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi);  // d2 in [0, 2q)
+        x[r] = csub(t, mi.q);
+        st_b(ep.ext + kr, voff, csub(mont_mul<SP>(t, mi.r2, mi), mi.q));  // d2 R
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[r] = ld_b(data + GZ::k_reg(r), voff);
+    }
     const u32 lw = lds_idx<S>(w, GZ::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) lds[lw + GZ::k_reg(r) + (GZ::k_reg(r) >> 4)] = x[r];
@@ -355,10 +385,11 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI>
 __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
-  static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE, "ntt_pass epilogues");
-  static_assert(EPI == EPI_NONE || (!INV && !COLS), "epilogues follow a forward row pass");
+  static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE || EPI == PRO_TENSOR, "ntt_pass epilogues");
+  static_assert(EPI != EPI_COMBINE || (!INV && !COLS), "epilogues follow a forward row pass");
+  static_assert(EPI != PRO_TENSOR || (INV && !COLS), "the tensor prologue feeds an inverse row pass");
   using PG = PassGeo<LOG_N, S, COLS, INV>;
-  static_assert(EPI == EPI_NONE || PG::LAST, "epilogues run in the last pass");
+  static_assert(EPI != EPI_COMBINE || PG::LAST, "epilogues run in the last pass");
   constexpr int T = 1 << (S - LOGR);
   static_assert(LOGR == 4, "register tile is 16 words");
   extern __shared__ u64 lds[];
@@ -391,6 +422,17 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
     ep.pinv = a.e_pinv[limb];
     ep.add = (a.e_add_mask >> (poly & 1)) & 1;
   }
+  if constexpr (EPI == PRO_TENSOR) {
+    const size_t LN = (size_t)a.t_L << LOG_N;
+    const size_t o = ((size_t)poly * 2 * a.t_L + limb) << LOG_N;
+    ep.a0 = a.t_a + o;
+    ep.a1 = ep.a0 + LN;
+    ep.b0 = a.t_b + o;
+    ep.b1 = ep.b0 + LN;
+    ep.o0 = a.t_out + o;
+    ep.o1 = ep.o0 + LN;
+    ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
+  }
   if constexpr (SP && !INV) {
     // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)
     if (mi.q < (1ull << 60)) {
@@ -418,10 +460,14 @@ int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
 
 template <int LOG_N, int S, int W, bool COLS, int EPI = EPI_NONE>
 int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
-  if constexpr (EPI != EPI_NONE) {
+  if constexpr (EPI == EPI_COMBINE) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, false, true, EPI>(c, a, n_jobs)
                       : launch_one<LOG_N, S, W, COLS, false, false, EPI>(c, a, n_jobs);
+  } else if constexpr (EPI == PRO_TENSOR) {
+    if (!inv) return fhe_fail(c, FHE_ERR_INVALID, "tensor prologue on a forward pass");
+    return c->special ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
+                      : launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs);
   } else {
     if (c->special)
       return inv ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
@@ -530,6 +576,42 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
     } else {
       if ((rc = col_pass(c, a, false, n_jobs))) return rc;
       rc = row_pass<EPI_COMBINE>(c, a, false, n_jobs);
+    }
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
+// CKKS mul+relin front end: the tensor product fused into the first pass of
+// the inverse NTT of d2 (PRO_TENSOR).  a, b, out: [n][2][L][N] (out may alias
+// a or b); dc [n][L][N] receives INTT(d2); ext's own-digit slots receive d2 R.
+int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+  const u32 L = c->L, QP = c->L + c->K;
+  const size_t N = c->n;
+  const u32 per = 65535u;  // gridDim.y
+  for (u32 p0 = 0; p0 < n; p0 += per) {
+    const u32 np = std::min(per, n - p0);
+    NttArgs t{};
+    t.map = LimbMap{dc + (size_t)p0 * L * N, L, L, 0, L, 0, 0, np};
+    t.tw = c->d_tw_inv;
+    t.mods = c->d_mods;
+    t.ninv = c->d_ninv;
+    t.log_n = c->log_n;
+    t.t_a = a + (size_t)p0 * 2 * L * N;
+    t.t_b = b + (size_t)p0 * 2 * L * N;
+    t.t_out = out + (size_t)p0 * 2 * L * N;
+    t.t_ext = ext + (size_t)p0 * ndig * QP * N;
+    t.t_L = L;
+    t.t_QP = QP;
+    t.t_alpha = c->alpha;
+    t.t_ndig = ndig;
+    const u32 n_jobs = np * L;
+    int rc;
+    if (c->log_n <= 14) {
+      rc = single_pass<PRO_TENSOR>(c, t, true, n_jobs);
+    } else {
+      if ((rc = row_pass<PRO_TENSOR>(c, t, true, n_jobs))) return rc;
+      rc = col_pass(c, t, true, n_jobs);
     }
     if (rc) return rc;
   }

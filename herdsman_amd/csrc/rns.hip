@@ -299,30 +299,6 @@ __global__ void __launch_bounds__(EW_BLOCK) tensor_kernel(TensorArgs t, const Mo
   t.e2[ct * t.e2_ct + off] = mul_mod<SP>(a1, b1, m);
 }
 
-// CKKS ct x ct tensor fused with the key-switch preparation of d2:
-//   out[ct][0] = a0 b0, out[ct][1] = a0 b1 + a1 b0  (the relinearisation base)
-//   dc[ct] = d2 = a1 b1 (to be INTT'd in place), ext[ct][own digit] = d2 * R
-template <bool SP>
-__global__ void __launch_bounds__(EW_BLOCK) tensor_ks_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
-                                                             u64 *out, u64 *__restrict__ dc, u64 *__restrict__ ext,
-                                                             const ModInfo *mods, u32 L, u32 QP, u32 alpha,
-                                                             u32 ndig, u32 log_n) {
-  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const u32 ct = blockIdx.y / L, i = blockIdx.y % L, j = i / alpha;
-  const size_t N = (size_t)1 << log_n, LN = (size_t)L * N;
-  const ModInfo m = mods[i];
-  const size_t o = (size_t)ct * 2 * LN + (size_t)i * N + k;
-  const u64 a0 = ld_nt(a + o), a1 = ld_nt(a + o + LN), b0 = ld_nt(b + o), b1 = ld_nt(b + o + LN);
-  st_nt(out + o, mul_mod<SP>(a0, b0, m));
-  U128 s = mul128(a0, b1);
-  mac128(s, a1, b0);
-  st_nt(out + o + LN, reduce128<SP>(s, m));
-  const u64 t = mont_reduce<SP>(mul128(a1, b1), m);  // d2 / R in [0, 2q)
-  st_nt(dc + (size_t)ct * LN + (size_t)i * N + k, csub(mont_mul<SP>(t, m.r2, m), m.q));                 // d2
-  st_nt(ext + ((size_t)(ct * ndig + j) * QP + i) * N + k,
-        csub(mont_mul<SP>(mont_mul<SP>(t, m.r2, m), m.r2, m), m.q));  // d2 R
-}
-
 // Rotation input: (c0, c1) -> sigma_g, fused with the key-switch preparation:
 //   base[ct][0] = sigma(c0); dc[ct] = sigma(c1); ext[ct][own] = sigma(c1) * R.
 // NTT domain (CKKS): slot permutation; coefficient domain (BFV): signed gather.
@@ -530,13 +506,6 @@ int ks_prep_impl(fhe_ctx *c, const u64 *d, u32 d_stride, u64 *dc, u64 *ext, u32 
 }
 
 template <bool SP>
-int tensor_ks_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig) {
-  hipLaunchKernelGGL((tensor_ks_kernel<SP>), dim3(c->n / EW_BLOCK, n * c->L), dim3(EW_BLOCK), 0, c->stream, a, b, out,
-                     dc, ext, c->d_mods, c->L, c->L + c->K, c->alpha, ndig, c->log_n);
-  return fhe_check(c, hipGetLastError(), "tensor_ks_kernel");
-}
-
-template <bool SP>
 int automorph_ks_impl(fhe_ctx *c, const u64 *ct, u64 *base, u64 *dc, u64 *ext, u32 g, u32 n, u32 ndig, bool ntt) {
   dim3 grid(c->n / EW_BLOCK, n * c->L);
   const u32 QP = c->L + c->K;
@@ -657,16 +626,16 @@ static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
 }
 
 // Hybrid key switching on a PREPARED scratch (dc and the own-digit limbs of
-// ext filled by ks_prep / tensor_ks / automorph_ks).
+// ext filled by ks_prep / the tensor INTT prologue / automorph_ks).
 //   out : [n][2][L][N], out_b = (add_mask bit b ? base_b : 0) + KS(d)_b;
 //         base may alias out (element-wise).
 static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
-                         bool ntt_form) {
+                         bool ntt_form, bool dc_is_coef = false) {
   const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
   u64 *dc = w.dc, *ext = w.ext, *acc = w.acc, *conv = w.conv;
   int rc;
-  // 1. INTT d (CKKS)
-  if (ntt_form && (rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true))) return rc;
+  // 1. INTT d (CKKS), unless the producer already did (ntt_inv_tensor_launch)
+  if (ntt_form && !dc_is_coef && (rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true))) return rc;
   // 2. ModUp: every non-own limb of every digit
   if ((rc = SP_DISPATCH(c, modup_impl, c, dc, L, ext, n, ndig))) return rc;
   // 3. NTT the converted limbs (all limbs for BFV, whose own limbs are coefficient form)
@@ -696,14 +665,15 @@ int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u
   return keyswitch_run(c, w, ksk, base, out, n, add_mask, ntt_form);
 }
 
-// CKKS ct x ct: tensor (fused with the KS preparation of d2) + relinearise.
+// CKKS ct x ct: the tensor product (and the KS preparation of d2) runs inside
+// the first pass of INTT(d2) (ntt.hip PRO_TENSOR), then relinearise.
 int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n) {
   void *ws;
   int rc = ctx_workspace(c, keyswitch_ws_bytes(c, n), &ws);
   if (rc) return rc;
   const KsWs w = ks_layout(c, n, (u64 *)ws);
-  if ((rc = SP_DISPATCH(c, tensor_ks_impl, c, a, b, out, w.dc, w.ext, n, w.ndig))) return rc;
-  return keyswitch_run(c, w, rlk, out, out, n, 3u, true);
+  if ((rc = ntt_inv_tensor_launch(c, a, b, out, w.dc, w.ext, n, w.ndig))) return rc;
+  return keyswitch_run(c, w, rlk, out, out, n, 3u, true, true);
 }
 
 // Rotation: automorphism (fused with the KS preparation of sigma(c1)) + KS.
