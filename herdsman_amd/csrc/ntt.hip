@@ -272,6 +272,18 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, GI + 1>(x, tn, lds, tw, data, voff, w, ts, hi, a, mi,
                                                                      mod, ep);
   } else {
+    // EPI_COMBINE: the epilogue's acc and base words are in flight while the
+    // last group computes (the LDS footprint caps occupancy at 4 waves per
+    // SIMD, so the 128-VGPR budget has room for them)
+    constexpr int RE = EPI == EPI_COMBINE ? R : 1;
+    u64 pa[RE], pb[RE];
+    if constexpr (EPI == EPI_COMBINE) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        pa[r] = ld_b(ep.acc + Grp<S, LOGR, 0>::k_reg(r), voff);
+        pb[r] = ep.add ? ld_b(ep.base + Grp<S, LOGR, 0>::k_reg(r), voff) : 0;
+      }
+    }
     run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
     if constexpr (PG::LAST) {
       if constexpr (!INV) {
@@ -302,8 +314,8 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
         const u64 v = lds[lr + kr + (kr >> 4)];
         if constexpr (EPI == EPI_COMBINE) {
           // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM
-          u64 ks = harvey_csub(mont_mul<SP>(sub_mod(ld_b(ep.acc + kr, voff), v, q), ep.pinv, mi), 0 - q);
-          if (ep.add) ks = add_mod(ks, ld_b(ep.base + kr, voff), q);
+          u64 ks = harvey_csub(mont_mul<SP>(sub_mod(pa[r], v, q), ep.pinv, mi), 0 - q);
+          if (ep.add) ks = add_mod(ks, pb[r], q);
           st_b(ep.out + kr, voff, ks);
         } else {
           st_b(data + kr, voff, v);
