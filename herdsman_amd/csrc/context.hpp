@@ -90,6 +90,7 @@ u64 host_to_mont(u64 x, u64 q);  // x * 2^64 mod q
 int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse);
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask);
+int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);
 // RNS kernels (rns.hip)
 enum class EwOp { Add, Sub, Mul };

@@ -54,11 +54,16 @@ struct NttArgs {
   u64 *t_out;            // may alias t_a / t_b (element-wise)
   u64 *t_ext;            // [ct][ndig][QP][N]
   u32 t_L, t_QP, t_alpha, t_ndig;
+  // PRO_AUTOMORPH (first pass of the inverse NTT of sigma_g(c1) in CKKS
+  // rotation): reads the input ciphertext t_a [ct][2][L][N] (NTT form) at the
+  // permuted slots, writes the key-switch base t_out[ct][0] = sigma_g(c0) and
+  // the own-digit ext slot sigma_g(c1) R, and transforms sigma_g(c1)
+  u32 t_g;
 };
 
 // EPI_COMBINE: epilogue of a forward last pass; PRO_TENSOR: prologue of an
 // inverse first (row) pass
-enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2 };
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3 };
 
 // per-workgroup epilogue / prologue operands (resolved once per limb)
 struct EpiRow {
@@ -69,6 +74,7 @@ struct EpiRow {
   bool add;
   const u64 *a0, *a1, *b0, *b1;  // PRO_TENSOR
   u64 *o0, *o1, *ext;
+  u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base; ext)
 };
 
 // LDS slot of element k of sub-transform w: one pad word per 16 words and per
@@ -363,6 +369,22 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         x[r] = csub(t, mi.q);
         st_b(ep.ext + kr, voff, csub(mont_mul<SP>(t, mi.r2, mi), mi.q));  // d2 R
       }
+    } else if constexpr (EPI == PRO_AUTOMORPH) {
+      // NTT-domain automorphism: slot k holds a(psi^e), e = 2 brv(k) + 1, and
+      // sigma_g(a)(psi^e) = a(psi^(e g)).  The 64 lanes of a load read one
+      // aligned 64-slot block of the source (g only permutes inside it).
+      constexpr u32 MASK = (2u << LOG_N) - 1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32 kr = GZ::k_reg(r);
+        const u32 k = (voff >> 3) + kr;
+        const u32 e = (((__brev(k) >> (32 - LOG_N)) << 1) | 1) * ep.g & MASK;
+        const u32 src = (__brev(e >> 1) >> (32 - LOG_N)) << 3;
+        const u64 y0 = ld_b(ep.a0, src), y1 = ld_b(ep.a1, src);
+        st_b(ep.o0 + kr, voff, y0);
+        x[r] = y1;
+        st_b(ep.ext + kr, voff, csub(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
+      }
     } else {
 #pragma unroll
       for (int r = 0; r < R; ++r) x[r] = ld_b(data + GZ::k_reg(r), voff);
@@ -397,9 +419,10 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI>
 __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
-  static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE || EPI == PRO_TENSOR, "ntt_pass epilogues");
+  static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH,
+                "ntt_pass epilogues");
   static_assert(EPI != EPI_COMBINE || (!INV && !COLS), "epilogues follow a forward row pass");
-  static_assert(EPI != PRO_TENSOR || (INV && !COLS), "the tensor prologue feeds an inverse row pass");
+  static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH) || (INV && !COLS), "prologues feed an inverse row pass");
   using PG = PassGeo<LOG_N, S, COLS, INV>;
   static_assert(EPI != EPI_COMBINE || PG::LAST, "epilogues run in the last pass");
   constexpr int T = 1 << (S - LOGR);
@@ -445,6 +468,15 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
     ep.o1 = ep.o0 + LN;
     ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
   }
+  if constexpr (EPI == PRO_AUTOMORPH) {
+    const size_t LN = (size_t)a.t_L << LOG_N;
+    const size_t o = ((size_t)poly * 2 * a.t_L + limb) << LOG_N;
+    ep.a0 = a.t_a + o;
+    ep.a1 = ep.a0 + LN;
+    ep.o0 = a.t_out + o;
+    ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
+    ep.g = a.t_g;
+  }
   if constexpr (SP && !INV) {
     // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)
     if (mi.q < (1ull << 60)) {
@@ -476,8 +508,8 @@ int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, false, true, EPI>(c, a, n_jobs)
                       : launch_one<LOG_N, S, W, COLS, false, false, EPI>(c, a, n_jobs);
-  } else if constexpr (EPI == PRO_TENSOR) {
-    if (!inv) return fhe_fail(c, FHE_ERR_INVALID, "tensor prologue on a forward pass");
+  } else if constexpr (EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH) {
+    if (!inv) return fhe_fail(c, FHE_ERR_INVALID, "prologue on a forward pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
                       : launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs);
   } else {
@@ -626,6 +658,38 @@ int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 
       rc = col_pass(c, t, true, n_jobs);
     }
     if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
+// CKKS rotation front end: the NTT-domain automorphism sigma_g (and the KS
+// preparation of sigma_g(c1)) fused into the first pass of its inverse NTT
+// (PRO_AUTOMORPH).  ct [n][2][L][N] must not alias base; base[ct][0] receives
+// sigma_g(c0), dc INTT(sigma_g(c1)), ext's own-digit slots sigma_g(c1) R.
+int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+  const u32 L = c->L, QP = c->L + c->K;
+  const size_t N = c->n;
+  if (c->log_n <= 14) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "automorphism prologue: log_n");
+  const u32 per = 65535u;  // gridDim.y
+  for (u32 p0 = 0; p0 < n; p0 += per) {
+    const u32 np = std::min(per, n - p0);
+    NttArgs t{};
+    t.map = LimbMap{dc + (size_t)p0 * L * N, L, L, 0, L, 0, 0, np};
+    t.tw = c->d_tw_inv;
+    t.mods = c->d_mods;
+    t.ninv = c->d_ninv;
+    t.log_n = c->log_n;
+    t.t_a = ct + (size_t)p0 * 2 * L * N;
+    t.t_out = base + (size_t)p0 * 2 * L * N;
+    t.t_ext = ext + (size_t)p0 * ndig * QP * N;
+    t.t_L = L;
+    t.t_QP = QP;
+    t.t_alpha = c->alpha;
+    t.t_ndig = ndig;
+    t.t_g = g & ((2u << c->log_n) - 1);
+    int rc;
+    if ((rc = row_pass<PRO_AUTOMORPH>(c, t, true, np * L))) return rc;
+    if ((rc = col_pass(c, t, true, np * L))) return rc;
   }
   return FHE_OK;
 }

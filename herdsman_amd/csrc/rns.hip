@@ -684,6 +684,11 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
   if (rc) return rc;
   u64 *base = (u64 *)ws;  // [n][2][L][N], poly 0 = sigma(c0)
   const KsWs w = ks_layout(c, n, base + n * 2 * LN);
+  if (ntt_form && c->log_n > 14) {
+    // CKKS at two-pass sizes: the automorphism runs inside the first pass of INTT(sigma(c1))
+    if ((rc = ntt_inv_automorph_launch(c, ct, g, base, w.dc, w.ext, n, w.ndig))) return rc;
+    return keyswitch_run(c, w, gk, base, out, n, 1u, true, true);
+  }
   if ((rc = SP_DISPATCH(c, automorph_ks_impl, c, ct, base, w.dc, w.ext, g, n, w.ndig, ntt_form))) return rc;
   return keyswitch_run(c, w, gk, base, out, n, 1u, ntt_form);
 }
