@@ -58,6 +58,9 @@ struct fhe_ctx {
   u32 log_n = 0, n = 0, L = 0, K = 0, dnum = 0, alpha = 0, nB = 0, nmod = 0;
   u64 t = 0;
   bool special = false;        // every modulus = 1 mod 2^32 (fast Montgomery)
+  // CKKS: the ModUp / ModDown conversion constants carry N^-1, so the inverse
+  // NTTs that feed them (INTT(d), INTT(acc_P)) skip their scaling
+  bool fold_ninv = false;
   std::vector<u64> moduli;
   // device-resident tables (constants in Montgomery form, x * 2^64 mod q)
   ModInfo *d_mods = nullptr;   // [nmod]
@@ -80,14 +83,15 @@ int fhe_fail(fhe_ctx *c, int code, const std::string &msg);
 int fhe_check(fhe_ctx *c, hipError_t e, const char *what);
 void *ctx_upload(fhe_ctx *c, const void *host, size_t bytes);  // owned blob
 int ctx_workspace(fhe_ctx *c, size_t bytes, void **out);
-ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst, int r_exp);
+ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst, int r_exp,
+                      bool fold_ninv = false);
 // host modular helpers
 u64 host_mulmod(u64 a, u64 b, u64 q);
 u64 host_inv(u64 a, u64 q);
 u64 host_to_mont(u64 x, u64 q);  // x * 2^64 mod q
 
 // NTT (ntt.hip)
-int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse);
+int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false);
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask);
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);

@@ -129,7 +129,10 @@ int ctx_workspace(fhe_ctx *c, size_t bytes, void **out) {
   return FHE_OK;
 }
 
-ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst, int r_exp) {
+// fold_ninv: the sources arrive as N * x (an inverse NTT without its N^-1), so
+// the per-source constant also carries N^-1
+ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst, int r_exp,
+                      bool fold_ninv) {
   ConvTab t{};
   t.ns = (u32)src.size();
   t.nd = (u32)dst.size();
@@ -140,7 +143,7 @@ ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector
     u64 prod = 1;
     for (u32 k = 0; k < t.ns; ++k)
       if (k != i) prod = hmul(prod, c->moduli[src[k]] % si, si);
-    hi[i] = tomont(hinv(prod, si), si);
+    hi[i] = tomont(fold_ninv ? hmul(hinv(prod, si), hinv((u64)c->n % si, si), si) : hinv(prod, si), si);
     for (u32 m = 0; m < t.nd; ++m) {
       const u64 dm = c->moduli[dst[m]];
       u64 p2 = 1;
@@ -206,6 +209,7 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
   }
   c->special = true;
   for (u64 q : c->moduli) c->special = c->special && ((q & 0xffffffffull) == 1);
+  c->fold_ninv = p->scheme == FHE_SCHEME_CKKS;
   const u32 n = c->n, nm = c->nmod;
   // per-modulus tables, constants in Montgomery form (x * 2^64 mod q)
   std::vector<ModInfo> mods(nm);
@@ -252,13 +256,13 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
       for (u32 i = lo; i < hi; ++i) src.push_back(i);
       for (u32 i = 0; i < QP; ++i)
         if (i < lo || i >= hi) dst.push_back(i);
-      tabs.push_back(make_conv_tab(c, src, dst, 2));  // ModUp output carries a factor R
+      tabs.push_back(make_conv_tab(c, src, dst, 2, c->fold_ninv));  // ModUp output carries a factor R
     }
     c->d_modup = (ConvTab *)ctx_upload(c, tabs.data(), sizeof(ConvTab) * tabs.size());
     std::vector<u32> src, dst;
     for (u32 k = 0; k < c->K; ++k) src.push_back(L + k);
     for (u32 i = 0; i < L; ++i) dst.push_back(i);
-    c->moddown = make_conv_tab(c, src, dst, 1);
+    c->moddown = make_conv_tab(c, src, dst, 1, c->fold_ninv);
     if (!c->d_pinv || !c->d_modup || !c->moddown.h) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
   }
   if (p->scheme == FHE_SCHEME_BFV) {

@@ -37,6 +37,9 @@ struct NttArgs {
   const ModInfo *mods;   // [nmod]
   const u64 *ninv;       // [nmod], N^-1 in Montgomery form
   u32 log_n;
+  // inverse only: leave out the N^-1 scaling (the consumer's conversion
+  // constants carry it, fhe_ctx::fold_ninv); outputs stay canonical
+  u32 noscale;
   // EPI_COMBINE (forward last pass over the ModDown conversion conv [p][L][N],
   // p = 2 ct + b): out[p][i] = (add_mask bit b ? base[p][i] : 0) + (acc[p][i] - conv) P^-1
   const u64 *e_acc;      // [p][e_acc_stride][N]
@@ -300,9 +303,14 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
           x[r] = harvey_csub(harvey_csub(v, 0 - q2), 0 - q);
         }
       } else {
-        const u64 sc = a.ninv[mod];
+        if (a.noscale) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) x[r] = harvey_csub(mont_mul<SP>(x[r], sc, mi), 0 - q);
+          for (int r = 0; r < R; ++r) x[r] = harvey_csub(x[r], 0 - q);  // GS outputs are below 2q
+        } else {
+          const u64 sc = a.ninv[mod];
+#pragma unroll
+          for (int r = 0; r < R; ++r) x[r] = harvey_csub(mont_mul<SP>(x[r], sc, mi), 0 - q);
+        }
       }
     }
     if constexpr (!COLS && G != 0) {
@@ -557,7 +565,7 @@ int row_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
 
 }  // namespace
 
-int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse) {
+int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale) {
   const u32 n_jobs = m.n_polys * m.cnt;
   if (n_jobs == 0) return FHE_OK;
   if (m.n_polys > 65535u) {
@@ -567,7 +575,7 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse) {
       LimbMap sub = m;
       sub.base = m.base + (size_t)p0 * m.poly_stride * c->n;
       sub.n_polys = (m.n_polys - p0) < per ? (m.n_polys - p0) : per;
-      int rc = ntt_launch(c, sub, inverse);
+      int rc = ntt_launch(c, sub, inverse, noscale);
       if (rc) return rc;
     }
     return FHE_OK;
@@ -578,6 +586,7 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse) {
   a.mods = c->d_mods;
   a.ninv = c->d_ninv;
   a.log_n = c->log_n;
+  a.noscale = inverse && noscale;
   if (c->log_n <= 14) return single_pass(c, a, inverse, n_jobs);
   int rc;
   if (!inverse) {
@@ -649,6 +658,7 @@ int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 
     t.t_QP = QP;
     t.t_alpha = c->alpha;
     t.t_ndig = ndig;
+    t.noscale = c->fold_ninv;  // dc feeds ModUp only
     const u32 n_jobs = np * L;
     int rc;
     if (c->log_n <= 14) {
@@ -687,6 +697,7 @@ int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *d
     t.t_alpha = c->alpha;
     t.t_ndig = ndig;
     t.t_g = g & ((2u << c->log_n) - 1);
+    t.noscale = c->fold_ninv;  // dc feeds ModUp only
     int rc;
     if ((rc = row_pass<PRO_AUTOMORPH>(c, t, true, np * L))) return rc;
     if ((rc = col_pass(c, t, true, np * L))) return rc;

@@ -635,7 +635,7 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   u64 *dc = w.dc, *ext = w.ext, *acc = w.acc, *conv = w.conv;
   int rc;
   // 1. INTT d (CKKS), unless the producer already did (ntt_inv_tensor_launch)
-  if (ntt_form && !dc_is_coef && (rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true))) return rc;
+  if (ntt_form && !dc_is_coef && (rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true, c->fold_ninv))) return rc;
   // 2. ModUp: every non-own limb of every digit
   if ((rc = SP_DISPATCH(c, modup_impl, c, dc, L, ext, n, ndig))) return rc;
   // 3. NTT the converted limbs (all limbs for BFV, whose own limbs are coefficient form)
@@ -648,7 +648,9 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   // 4. inner product with the key
   if ((rc = SP_DISPATCH(c, inner_impl, c, ext, ksk, acc, n, ndig))) return rc;
   // 5. ModDown: INTT the P part (all of Q u P for BFV), convert P -> Q
-  if ((rc = ntt_launch(c, LimbMap{acc, QP, ntt_form ? K : QP, ntt_form ? L : 0, QP, 0, 0, 2 * n}, true))) return rc;
+  if ((rc = ntt_launch(c, LimbMap{acc, QP, ntt_form ? K : QP, ntt_form ? L : 0, QP, 0, 0, 2 * n}, true,
+                       ntt_form && c->fold_ninv)))
+    return rc;
   if ((rc = conv_launch(c, c->moddown, acc + (size_t)L * N, QP, conv, L, 2 * n))) return rc;
   // 6. combine: fused into the last pass of NTT(conv) for NTT-form results
   if (ntt_form) return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask);
@@ -717,7 +719,8 @@ int behz_setup(fhe_ctx *c) {
       if (k != i) { qh = M(qh, qq[k] % qq[i], qq[i]); hm = (hm * (qq[k] & 0xffffffffull)) & 0xffffffffull; }
     const u64 hinv = host_inv(qh, qq[i]);
     B->mt_hinv_R[i] = R(M(hinv, mt % qq[i], qq[i]), qq[i]);
-    B->t_hinv_R[i] = R(M(hinv, c->t % qq[i], qq[i]), qq[i]);
+    // the floor's inputs come from an inverse NTT without its N^-1 (bfv_mul_relin_impl): fold it here
+    B->t_hinv_R[i] = R(M(M(hinv, c->t % qq[i], qq[i]), host_inv(c->n % qq[i], qq[i]), qq[i]), qq[i]);
     B->h_mod_mt[i] = (u32)hm;
     for (u32 j = 0; j < nB; ++j) {
       u64 p2 = 1;
@@ -740,7 +743,7 @@ int behz_setup(fhe_ctx *c) {
     B->q_mod_bsk_R[j] = R(qmb, b);
     B->inv_q_bsk_R[j] = R(host_inv(qmb, b), b);
     B->inv_mt_bsk_R[j] = R(host_inv(mt % b, b), b);
-    B->t_bsk_R[j] = R(c->t % b, b);
+    B->t_bsk_R[j] = R(M(c->t % b, host_inv(c->n % b, b), b), b);
   }
   for (u32 j = 0; j + 1 < nB; ++j) {
     u64 bh = 1, bhm = 1;
@@ -790,8 +793,9 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   if ((rc = tensor_launch(c, xb, 4 * BN, BN, xb + 2 * BN, 4 * BN, BN, eb, 3 * BN, BN, eb + 2 * BN, 3 * BN, n, nB,
                           bsk0)))
     return rc;
-  if ((rc = ntt_launch(c, LimbMap{eq, L, L, 0, L, 0, 0, 3 * n}, true))) return rc;
-  if ((rc = ntt_launch(c, LimbMap{eb, nB, nB, 0, nB, 0, bsk0, 3 * n}, true))) return rc;
+  // (unscaled: behz_floor's t constants carry N^-1)
+  if ((rc = ntt_launch(c, LimbMap{eq, L, L, 0, L, 0, 0, 3 * n}, true, true))) return rc;
+  if ((rc = ntt_launch(c, LimbMap{eb, nB, nB, 0, nB, 0, bsk0, 3 * n}, true, true))) return rc;
   // 5. scale and round: r0, r1 -> out, r2 -> workspace
   if ((rc = SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, r2, n))) return rc;
   // 6. relinearize r2 and add to (r0, r1)

@@ -554,3 +554,21 @@ def test_conjugation_and_identity_galois(hb, scheme):
     for g in (2 * o.n - 1, 1):
         c.rotate(hb.to_device(ct), g, hb.to_device(gk), dout)
         assert np.array_equal(hb.to_host(dout), o.rotate(ct, g, gk)), g
+
+
+@pytest.mark.parametrize("log_n,L,K,dnum", [(15, 5, 2, 2), (17, 3, 1, 3)])
+def test_ckks_rotate_fused_automorphism(hb, log_n, L, K, dnum):
+    """Two-pass sizes run the automorphism inside the first INTT pass (PRO_AUTOMORPH):
+    generic rotations, conjugation (2N-1), identity (1), and an in-place call."""
+    o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum)
+    ct = o.uniform((2, 2, L, 1 << log_n), seed=150 + log_n)
+    gk = o.uniform(o.key_shape(), seed=151 + log_n)
+    dgk = hb.to_device(gk)
+    dout = hb.empty(ct.shape)
+    for g in (o.galois_elt(1), o.galois_elt(-5), 2 * o.n - 1, 1):
+        c.rotate(hb.to_device(ct), g, dgk, dout)
+        assert np.array_equal(hb.to_host(dout), o.rotate(ct, g, gk)), g
+    g = o.galois_elt(7)
+    dct = hb.to_device(ct)
+    c.rotate(dct, g, dgk, dct)
+    assert np.array_equal(hb.to_host(dct), o.rotate(ct, g, gk))
