@@ -66,7 +66,9 @@ struct NttArgs {
 
 // EPI_COMBINE: epilogue of a forward last pass; PRO_TENSOR: prologue of an
 // inverse first (row) pass
-enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3 };
+// PRO_BFVT: prologue of the inverse first (row) pass of the BFV tensor
+// product e = (a0 b0, a0 b1 + a1 b0, a1 b1) in one RNS base
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4 };
 
 // per-workgroup epilogue / prologue operands (resolved once per limb)
 struct EpiRow {
@@ -78,6 +80,7 @@ struct EpiRow {
   const u64 *a0, *a1, *b0, *b1;  // PRO_TENSOR
   u64 *o0, *o1, *ext;
   u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base; ext)
+  u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is
 };
 
 // LDS slot of element k of sub-transform w: one pad word per 16 words and per
@@ -377,6 +380,24 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         x[r] = csub(t, mi.q);
         st_b(ep.ext + kr, voff, csub(mont_mul<SP>(t, mi.r2, mi), mi.q));  // d2 R
       }
+    } else if constexpr (EPI == PRO_BFVT) {
+      // the BFV tensor formulas at the coalesced positions; e is per workgroup
+      if (ep.e == 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32 kr = GZ::k_reg(r);
+          U128 s = mul128(ld_b(ep.a0 + kr, voff), ld_b(ep.b1 + kr, voff));
+          mac128(s, ld_b(ep.a1 + kr, voff), ld_b(ep.b0 + kr, voff));
+          x[r] = reduce128<SP>(s, mi);
+        }
+      } else {
+        // e = 0: (a0, b0), e = 2: (a1, b1) -- the pair is resolved in ntt_pass
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32 kr = GZ::k_reg(r);
+          x[r] = mul_mod<SP>(ld_b(ep.a0 + kr, voff), ld_b(ep.b0 + kr, voff), mi);
+        }
+      }
     } else if constexpr (EPI == PRO_AUTOMORPH) {
       // NTT-domain automorphism: slot k holds a(psi^e), e = 2 brv(k) + 1, and
       // sigma_g(a)(psi^e) = a(psi^(e g)).  The 64 lanes of a load read one
@@ -427,10 +448,12 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI>
 __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
-  static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH,
+  static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
+                    EPI == PRO_BFVT,
                 "ntt_pass epilogues");
   static_assert(EPI != EPI_COMBINE || (!INV && !COLS), "epilogues follow a forward row pass");
-  static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH) || (INV && !COLS), "prologues feed an inverse row pass");
+  static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT) || (INV && !COLS),
+                "prologues feed an inverse row pass");
   using PG = PassGeo<LOG_N, S, COLS, INV>;
   static_assert(EPI != EPI_COMBINE || PG::LAST, "epilogues run in the last pass");
   constexpr int T = 1 << (S - LOGR);
@@ -476,6 +499,16 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
     ep.o1 = ep.o0 + LN;
     ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
   }
+  if constexpr (EPI == PRO_BFVT) {
+    // poly = 3 ct + e; the inputs are x[ct][4][nl][N] = (a0, a1, b0, b1)
+    const size_t LN = (size_t)a.t_L << LOG_N;
+    const u64 *x0 = a.t_a + (((size_t)(poly / 3) * 4 * a.t_L + limb) << LOG_N);
+    ep.e = poly % 3;
+    ep.a0 = ep.e == 2 ? x0 + LN : x0;
+    ep.a1 = x0 + LN;
+    ep.b0 = ep.e == 2 ? x0 + 3 * LN : x0 + 2 * LN;
+    ep.b1 = x0 + 3 * LN;
+  }
   if constexpr (EPI == PRO_AUTOMORPH) {
     const size_t LN = (size_t)a.t_L << LOG_N;
     const size_t o = ((size_t)poly * 2 * a.t_L + limb) << LOG_N;
@@ -516,7 +549,7 @@ int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, false, true, EPI>(c, a, n_jobs)
                       : launch_one<LOG_N, S, W, COLS, false, false, EPI>(c, a, n_jobs);
-  } else if constexpr (EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH) {
+  } else if constexpr (EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH || EPI == PRO_BFVT) {
     if (!inv) return fhe_fail(c, FHE_ERR_INVALID, "prologue on a forward pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
                       : launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs);
@@ -701,6 +734,38 @@ int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *d
     int rc;
     if ((rc = row_pass<PRO_AUTOMORPH>(c, t, true, np * L))) return rc;
     if ((rc = col_pass(c, t, true, np * L))) return rc;
+  }
+  return FHE_OK;
+}
+
+// BFV mul+relin: the tensor product of x [n][4][nl][N] = (a0, a1, b0, b1), NTT
+// form, in the nl-limb base starting at modulus mod_offset, fused into the
+// first pass of its inverse NTT (PRO_BFVT); e [n][3][nl][N] receives the
+// coefficient-form products WITHOUT the N^-1 factor (behz_floor's constants
+// carry it).
+int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *x, u64 *e, u32 nl, u32 mod_offset, u32 n) {
+  const size_t N = c->n;
+  const u32 per = 65535u;  // gridDim.y, a multiple of 3
+  for (u32 p0 = 0; p0 < 3 * n; p0 += per) {
+    const u32 np = std::min(per, 3 * n - p0);
+    NttArgs t{};
+    t.map = LimbMap{e + (size_t)p0 * nl * N, nl, nl, 0, nl, 0, mod_offset, np};
+    t.tw = c->d_tw_inv;
+    t.mods = c->d_mods;
+    t.ninv = c->d_ninv;
+    t.log_n = c->log_n;
+    t.noscale = 1;
+    t.t_a = x + (size_t)(p0 / 3) * 4 * nl * N;
+    t.t_L = nl;
+    const u32 n_jobs = np * nl;
+    int rc;
+    if (c->log_n <= 14) {
+      rc = single_pass<PRO_BFVT>(c, t, true, n_jobs);
+    } else {
+      if ((rc = row_pass<PRO_BFVT>(c, t, true, n_jobs))) return rc;
+      rc = col_pass(c, t, true, n_jobs);
+    }
+    if (rc) return rc;
   }
   return FHE_OK;
 }

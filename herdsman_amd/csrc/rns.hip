@@ -270,35 +270,6 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_combine_kernel(const u64 *__restr
   out[o] = ks;
 }
 
-// CKKS tensor (orc_mul_relin): d0 = a0 b0, d1 = a0 b1 + a1 b0, d2 = a1 b1.
-// Generic strides so BFV reuses it on Q and on Bsk.
-struct TensorArgs {
-  const u64 *a;
-  const u64 *b;
-  u64 *e01;
-  u64 *e2;
-  size_t a_ct, a_poly;   // strides in words
-  size_t b_ct, b_poly;
-  size_t e_ct, e_poly;
-  size_t e2_ct;
-  u32 nl, mod_offset, log_n;
-};
-template <bool SP>
-__global__ void __launch_bounds__(EW_BLOCK) tensor_kernel(TensorArgs t, const ModInfo *mods) {
-  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const u32 ct = blockIdx.y / t.nl, l = blockIdx.y % t.nl;
-  const size_t off = ((size_t)l << t.log_n) + k;
-  const ModInfo m = mods[t.mod_offset + l];
-  const u64 *A = t.a + ct * t.a_ct + off, *B = t.b + ct * t.b_ct + off;
-  const u64 a0 = A[0], a1 = A[t.a_poly], b0 = B[0], b1 = B[t.b_poly];
-  u64 *E = t.e01 + ct * t.e_ct + off;
-  E[0] = mul_mod<SP>(a0, b0, m);
-  U128 s = mul128(a0, b1);
-  mac128(s, a1, b0);
-  E[t.e_poly] = reduce128<SP>(s, m);
-  t.e2[ct * t.e2_ct + off] = mul_mod<SP>(a1, b1, m);
-}
-
 // Rotation input: (c0, c1) -> sigma_g, fused with the key-switch preparation:
 //   base[ct][0] = sigma(c0); dc[ct] = sigma(c1); ext[ct][own] = sigma(c1) * R.
 // NTT domain (CKKS): slot permutation; coefficient domain (BFV): signed gather.
@@ -531,12 +502,6 @@ int combine_impl(fhe_ctx *c, const u64 *acc, const u64 *conv, const u64 *base, u
 }
 
 template <bool SP>
-int tensor_impl(fhe_ctx *c, const TensorArgs &t, u32 jobs) {
-  hipLaunchKernelGGL((tensor_kernel<SP>), dim3(c->n / EW_BLOCK, jobs), dim3(EW_BLOCK), 0, c->stream, t, c->d_mods);
-  return fhe_check(c, hipGetLastError(), "tensor_kernel");
-}
-
-template <bool SP>
 int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xq, u64 *xb, u32 n) {
   dim3 grid(c->n / EW_BLOCK, 4 * n);
   const BehzDev *bz = (const BehzDev *)c->behz;
@@ -695,11 +660,6 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
   return keyswitch_run(c, w, gk, base, out, n, 1u, ntt_form);
 }
 
-int tensor_launch(fhe_ctx *c, const u64 *a, size_t a_ct, size_t a_poly, const u64 *b, size_t b_ct, size_t b_poly,
-                  u64 *e01, size_t e_ct, size_t e_poly, u64 *e2, size_t e2_ct, u32 n_ct, u32 nl, u32 mod_offset) {
-  TensorArgs t{a, b, e01, e2, a_ct, a_poly, b_ct, b_poly, e_ct, e_poly, e2_ct, nl, mod_offset, c->log_n};
-  return SP_DISPATCH(c, tensor_impl, c, t, n_ct * nl);
-}
 
 // ------------------------------------------------------------ BEHZ setup
 int behz_setup(fhe_ctx *c) {
@@ -781,21 +741,15 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   u64 *eb = eq + (size_t)n * 3 * L * N;       // [n][3][nB][N]
   u64 *r2 = eb + (size_t)n * 3 * nB * N;      // [n][L][N]
   u64 *ksws = r2 + (size_t)n * L * N;
-  const size_t LN = (size_t)L * N, BN = (size_t)nB * N;
   // 1-2. gather a0,a1,b0,b1 per item into xq and extend them to Bsk (coefficient form)
   if ((rc = SP_DISPATCH(c, behz_extend_impl, c, a, b, xq, xb, n))) return rc;
   // 3. NTT in Q and Bsk
   if ((rc = ntt_launch(c, LimbMap{xq, L, L, 0, L, 0, 0, 4 * n}, false))) return rc;
   if ((rc = ntt_launch(c, LimbMap{xb, nB, nB, 0, nB, 0, bsk0, 4 * n}, false))) return rc;
-  // 4. tensor in both bases
-  if ((rc = tensor_launch(c, xq, 4 * LN, LN, xq + 2 * LN, 4 * LN, LN, eq, 3 * LN, LN, eq + 2 * LN, 3 * LN, n, L, 0)))
-    return rc;
-  if ((rc = tensor_launch(c, xb, 4 * BN, BN, xb + 2 * BN, 4 * BN, BN, eb, 3 * BN, BN, eb + 2 * BN, 3 * BN, n, nB,
-                          bsk0)))
-    return rc;
-  // (unscaled: behz_floor's t constants carry N^-1)
-  if ((rc = ntt_launch(c, LimbMap{eq, L, L, 0, L, 0, 0, 3 * n}, true, true))) return rc;
-  if ((rc = ntt_launch(c, LimbMap{eb, nB, nB, 0, nB, 0, bsk0, 3 * n}, true, true))) return rc;
+  // 4. tensor in both bases, fused into the first pass of its inverse NTT
+  //    (unscaled: behz_floor's t constants carry N^-1)
+  if ((rc = ntt_inv_bfv_tensor_launch(c, xq, eq, L, 0, n))) return rc;
+  if ((rc = ntt_inv_bfv_tensor_launch(c, xb, eb, nB, bsk0, n))) return rc;
   // 5. scale and round: r0, r1 -> out, r2 -> workspace
   if ((rc = SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, r2, n))) return rc;
   // 6. relinearize r2 and add to (r0, r1)
