@@ -572,3 +572,18 @@ def test_ckks_rotate_fused_automorphism(hb, log_n, L, K, dnum):
     dct = hb.to_device(ct)
     c.rotate(dct, g, dgk, dct)
     assert np.array_equal(hb.to_host(dct), o.rotate(ct, g, gk))
+
+
+@pytest.mark.parametrize("log_n,L,K,dnum", [(16, 3, 2, 3), (17, 2, 1, 2)])
+def test_bfv_mul_relin_fused_tensor_sizes(hb, log_n, L, K, dnum):
+    """The BFV tensor product runs inside the first pass of INTT(eq)/INTT(eb)
+    (PRO_BFVT) at every two-pass ring size; 3 products so every (ct, e) poly
+    index is hit, plus an in-place call (out aliases a)."""
+    o, c = pair(hb, SCHEME_BFV, log_n, L, K, dnum, t=65537)
+    a = o.uniform((3, 2, L, 1 << log_n), seed=160 + log_n)
+    b = o.uniform((3, 2, L, 1 << log_n), seed=161 + log_n)
+    rlk = o.uniform(o.key_shape(), seed=162 + log_n)
+    want = o.mul_relin(a, b, rlk)
+    da = hb.to_device(a)
+    c.mul_relin(da, hb.to_device(b), hb.to_device(rlk), da)
+    assert np.array_equal(hb.to_host(da), want)
