@@ -91,7 +91,8 @@ u64 host_inv(u64 a, u64 q);
 u64 host_to_mont(u64 x, u64 q);  // x * 2^64 mod q
 
 // NTT (ntt.hip)
-int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false);
+// noscale (inverse): no N^-1 multiply; lazy_out (forward): outputs below 8q, not canonical
+int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false, bool lazy_out = false);
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask);
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *x, u64 *e, u32 nl, u32 mod_offset, u32 n);

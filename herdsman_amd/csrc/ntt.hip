@@ -40,6 +40,10 @@ struct NttArgs {
   // inverse only: leave out the N^-1 scaling (the consumer's conversion
   // constants carry it, fhe_ctx::fold_ninv); outputs stay canonical
   u32 noscale;
+  // forward only: leave the outputs in the lazy range (below 8q < 2^63), for a
+  // consumer whose Montgomery products accept any input below 2^63 (the KS
+  // inner product on special moduli)
+  u32 lazy_out;
   // EPI_COMBINE (forward last pass over the ModDown conversion conv [p][L][N],
   // p = 2 ct + b): out[p][i] = (add_mask bit b ? base[p][i] : 0) + (acc[p][i] - conv) P^-1
   const u64 *e_acc;      // [p][e_acc_stride][N]
@@ -299,11 +303,13 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
     if constexpr (PG::LAST) {
       if constexpr (!INV) {
+        if (!a.lazy_out) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          u64 v = x[r];
-          if (WIDE) v = harvey_csub(v, 0 - 2 * q2);
-          x[r] = harvey_csub(harvey_csub(v, 0 - q2), 0 - q);
+          for (int r = 0; r < R; ++r) {
+            u64 v = x[r];
+            if (WIDE) v = harvey_csub(v, 0 - 2 * q2);
+            x[r] = harvey_csub(harvey_csub(v, 0 - q2), 0 - q);
+          }
         }
       } else {
         if (a.noscale) {
@@ -598,7 +604,7 @@ int row_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
 
 }  // namespace
 
-int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale) {
+int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool lazy_out) {
   const u32 n_jobs = m.n_polys * m.cnt;
   if (n_jobs == 0) return FHE_OK;
   if (m.n_polys > 65535u) {
@@ -608,7 +614,7 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale) {
       LimbMap sub = m;
       sub.base = m.base + (size_t)p0 * m.poly_stride * c->n;
       sub.n_polys = (m.n_polys - p0) < per ? (m.n_polys - p0) : per;
-      int rc = ntt_launch(c, sub, inverse, noscale);
+      int rc = ntt_launch(c, sub, inverse, noscale, lazy_out);
       if (rc) return rc;
     }
     return FHE_OK;
@@ -620,6 +626,7 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale) {
   a.ninv = c->d_ninv;
   a.log_n = c->log_n;
   a.noscale = inverse && noscale;
+  a.lazy_out = !inverse && lazy_out;
   if (c->log_n <= 14) return single_pass(c, a, inverse, n_jobs);
   int rc;
   if (!inverse) {

@@ -608,7 +608,9 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
     const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
     LimbMap m{ext + (size_t)j * QP * N, ndig * QP, ntt_form ? QP - (hi - lo) : QP, 0,
               ntt_form ? lo : QP, ntt_form ? hi - lo : 0, 0, n};
-    if ((rc = ntt_launch(c, m, false))) return rc;
+    // special moduli: the inner product's Montgomery products take the lazy
+    // (< 8q) NTT outputs as they are, so the last pass skips canonicalising
+    if ((rc = ntt_launch(c, m, false, false, c->special))) return rc;
   }
   // 4. inner product with the key
   if ((rc = SP_DISPATCH(c, inner_impl, c, ext, ksk, acc, n, ndig))) return rc;
