@@ -97,8 +97,12 @@ struct EpiRow {
 __device__ __forceinline__ u64 ld_at(const u64 *base, u32 idx) {
   return *(const u64 *)((const char *)base + (idx << 3));
 }
-// the same at a byte offset (per-thread offsets computed once per pass)
-__device__ __forceinline__ u64 ld_b(const u64 *base, u32 off) { return *(const u64 *)((const char *)base + off); }
+// the same at a byte offset (per-thread offsets computed once per pass); data
+// words are read once per pass, so the loads are non-temporal (+1% on the
+// forward NTT and the headline step, A/B on one box; nt stores measured neutral)
+__device__ __forceinline__ u64 ld_b(const u64 *base, u32 off) {
+  return __builtin_nontemporal_load((const u64 *)((const char *)base + off));
+}
 __device__ __forceinline__ void st_b(u64 *base, u32 off, u64 v) { *(u64 *)((char *)base + off) = v; }
 
 template <int S>
