@@ -97,10 +97,12 @@ struct EpiRow {
 __device__ __forceinline__ u64 ld_at(const u64 *base, u32 idx) {
   return *(const u64 *)((const char *)base + (idx << 3));
 }
-// the same at a byte offset (per-thread offsets computed once per pass); data
-// words are read once per pass, so the loads are non-temporal (+1% on the
-// forward NTT and the headline step, A/B on one box; nt stores measured neutral)
-__device__ __forceinline__ u64 ld_b(const u64 *base, u32 off) {
+// the same at a byte offset (per-thread offsets computed once per pass)
+__device__ __forceinline__ u64 ld_b(const u64 *base, u32 off) { return *(const u64 *)((const char *)base + off); }
+// a pass's own data words are read once: non-temporal (A/B on one box: the
+// forward NTT -1%; the fused prologue/epilogue operand streams lose with nt,
+// so they keep ld_b; nt stores measured neutral)
+__device__ __forceinline__ u64 ld_d(const u64 *base, u32 off) {
   return __builtin_nontemporal_load((const u64 *)((const char *)base + off));
 }
 __device__ __forceinline__ void st_b(u64 *base, u32 off, u64 v) { *(u64 *)((char *)base + off) = v; }
@@ -426,7 +428,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) x[r] = ld_b(data + GZ::k_reg(r), voff);
+      for (int r = 0; r < R; ++r) x[r] = ld_d(data + GZ::k_reg(r), voff);
     }
     const u32 lw = lds_idx<S>(w, GZ::k_thr(ts));
 #pragma unroll
@@ -443,7 +445,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
     using GF = Grp<S, LOGR, G0>;
     voff = (gb + (GF::k_thr(ts) << PG::LS)) << 3;
 #pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = ld_b(data + ((size_t)GF::k_reg(r) << PG::LS), voff);
+    for (int r = 0; r < R; ++r) x[r] = ld_d(data + ((size_t)GF::k_reg(r) << PG::LS), voff);
   }
   // the final store uses the group-0 layout for row passes and the last
   // group's layout for column passes; recompute the offset for the latter
