@@ -587,3 +587,21 @@ def test_bfv_mul_relin_fused_tensor_sizes(hb, log_n, L, K, dnum):
     da = hb.to_device(a)
     c.mul_relin(da, hb.to_device(b), hb.to_device(rlk), da)
     assert np.array_equal(hb.to_host(da), want)
+
+
+def test_generic_moduli_two_pass_fused_paths(hb):
+    """Generic (non 2^32) moduli at a two-pass size: the CKKS tensor and
+    automorphism prologues and the unscaled inverse NTTs on the generic
+    Montgomery path (BFV's tensor prologue: test_generic_moduli_ntt_and_bfv)."""
+    log_n, L, K, dnum = 15, 3, 2, 2
+    mods = np.array(_generic_primes(60, log_n, L + K), dtype=np.uint64)
+    o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum, moduli=mods)
+    a = o.uniform((2, 2, L, 1 << log_n), seed=170)
+    b = o.uniform((2, 2, L, 1 << log_n), seed=171)
+    k = o.uniform(o.key_shape(), seed=172)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(k), dout)
+    assert np.array_equal(hb.to_host(dout), o.mul_relin(a, b, k))
+    g = o.galois_elt(3)
+    c.rotate(hb.to_device(a), g, hb.to_device(k), dout)
+    assert np.array_equal(hb.to_host(dout), o.rotate(a, g, k))
