@@ -605,3 +605,29 @@ def test_generic_moduli_two_pass_fused_paths(hb):
     g = o.galois_elt(3)
     c.rotate(hb.to_device(a), g, hb.to_device(k), dout)
     assert np.array_equal(hb.to_host(dout), o.rotate(a, g, k))
+
+
+def test_concurrent_contexts_on_streams(hb):
+    """bench.py's configuration: several contexts, one HIP stream each, run
+    ct-mult+relin on slices of one batch concurrently with a shared key; every
+    slice must match the oracle (per-context workspaces, no cross-talk)."""
+    import torch
+
+    log_n, L, K, dnum, S, per = 15, 4, 2, 2, 4, 2
+    o, c0 = pair(hb, SCHEME_CKKS, log_n, L, K, dnum)
+    ctxs = [c0] + [hb.Context(SCHEME_CKKS, log_n, L, K, dnum, moduli=o.moduli) for _ in range(S - 1)]
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    for c, s in zip(ctxs, streams):
+        c.set_stream(s)
+    a = o.uniform((S * per, 2, L, 1 << log_n), seed=180)
+    b = o.uniform((S * per, 2, L, 1 << log_n), seed=181)
+    k = o.uniform(o.key_shape(), seed=182)
+    da, db, dk = hb.to_device(a), hb.to_device(b), hb.to_device(k)
+    dout = hb.empty(a.shape)
+    torch.cuda.synchronize()
+    for rep in range(2):
+        for i, c in enumerate(ctxs):
+            sl = slice(i * per, (i + 1) * per)
+            c.mul_relin(da[sl], db[sl], dk, dout[sl])
+    torch.cuda.synchronize()
+    assert np.array_equal(hb.to_host(dout), o.mul_relin(a, b, k))
