@@ -177,25 +177,52 @@ class Context:
     def key_shape(self):
         return (self.dnum, 2, self.L + self.K, self.n)
 
+    # ---- argument checks (the C ABI trusts its sizes: a short buffer would be
+    # read or written out of bounds on the GPU, so shapes and devices are
+    # checked here, before any pointer crosses the ABI)
+    def _on_device(self, *ts):
+        for t in ts:
+            if t.device.type != "cuda" or t.device.index != self.device:
+                raise FheBackendError(f"buffer on {t.device}, context on cuda:{self.device}")
+
+    def _ct_batch(self, *cts):
+        n = cts[0].shape[0] if cts[0].dim() == 4 else -1
+        for t in cts:
+            if tuple(t.shape) != self.ct_shape(n):
+                raise FheBackendError(f"ciphertext batch shape {tuple(t.shape)}, expected {self.ct_shape(max(n, 0))}")
+        self._on_device(*cts)
+        return n
+
+    def _key(self, k):
+        if tuple(k.shape) != self.key_shape():
+            raise FheBackendError(f"key shape {tuple(k.shape)}, expected {self.key_shape()}")
+        self._on_device(k)
+
     # ---- primitives
-    def _limbs(self, x):
-        nl = x.shape[-2]
-        if x.shape[-1] != self.n:
+    def _limbs(self, x, mod_begin: int = 0):
+        if x.dim() < 2 or x.shape[-1] != self.n:
             raise FheBackendError(f"last dim must be N={self.n}")
+        nl = x.shape[-2]
+        if mod_begin < 0 or nl < 1 or mod_begin + nl > len(self.moduli):
+            raise FheBackendError(f"limbs [{mod_begin}, {mod_begin + nl}) outside the {len(self.moduli)} moduli")
+        self._on_device(x)
         return x.numel() // (nl * self.n), nl
 
     def ntt_fwd(self, x, mod_begin: int = 0):
-        n, nl = self._limbs(x)
+        n, nl = self._limbs(x, mod_begin)
         self._ck(self.lib.fhe_ntt_fwd(self.h, _ptr(x), n, mod_begin, nl), "fhe_ntt_fwd")
         return x
 
     def ntt_inv(self, x, mod_begin: int = 0):
-        n, nl = self._limbs(x)
+        n, nl = self._limbs(x, mod_begin)
         self._ck(self.lib.fhe_ntt_inv(self.h, _ptr(x), n, mod_begin, nl), "fhe_ntt_inv")
         return x
 
     def poly_op(self, op: str, a, b, out, mod_begin: int = 0):
-        n, nl = self._limbs(a)
+        n, nl = self._limbs(a, mod_begin)
+        if b.shape != a.shape or out.shape != a.shape:
+            raise FheBackendError("poly_op operands must have one shape")
+        self._on_device(b, out)
         fn = {"add": self.lib.fhe_poly_add, "sub": self.lib.fhe_poly_sub, "mul": self.lib.fhe_poly_mul}[op]
         self._ck(fn(self.h, _ptr(a), _ptr(b), _ptr(out), n, mod_begin, nl), f"fhe_poly_{op}")
         return out
@@ -204,41 +231,60 @@ class Context:
         s = np.ascontiguousarray(src_mods, dtype=np.uint32)
         d = np.ascontiguousarray(dst_mods, dtype=np.uint32)
         n = src.numel() // (len(s) * self.n)
+        if src.numel() != n * len(s) * self.n or dst.numel() != n * len(d) * self.n:
+            raise FheBackendError("base_conv: src / dst sizes do not match the modulus lists")
+        self._on_device(src, dst)
         self._ck(self.lib.fhe_base_conv(self.h, _ptr(src), s.ctypes.data, len(s), _ptr(dst), d.ctypes.data,
                                         len(d), n), "fhe_base_conv")
         return dst
 
     def fill_uniform(self, x, seed: int, mod_begin: int = 0):
-        n, nl = self._limbs(x)
+        n, nl = self._limbs(x, mod_begin)
         self._ck(self.lib.fhe_fill_uniform(self.h, _ptr(x), n, mod_begin, nl, seed & (2**64 - 1)),
                  "fhe_fill_uniform")
         return x
 
     # ---- ciphertext ops
     def add(self, a, b, out):
-        self._ck(self.lib.fhe_add(self.h, _ptr(a), _ptr(b), _ptr(out), a.shape[0]), "fhe_add")
+        n = self._ct_batch(a, b, out)
+        self._ck(self.lib.fhe_add(self.h, _ptr(a), _ptr(b), _ptr(out), n), "fhe_add")
         return out
 
     def sub(self, a, b, out):
-        self._ck(self.lib.fhe_sub(self.h, _ptr(a), _ptr(b), _ptr(out), a.shape[0]), "fhe_sub")
+        n = self._ct_batch(a, b, out)
+        self._ck(self.lib.fhe_sub(self.h, _ptr(a), _ptr(b), _ptr(out), n), "fhe_sub")
         return out
 
     def mul_relin(self, a, b, rlk, out):
-        self._ck(self.lib.fhe_mul_relin(self.h, _ptr(a), _ptr(b), _ptr(rlk), _ptr(out), a.shape[0]),
-                 "fhe_mul_relin")
+        n = self._ct_batch(a, b, out)
+        self._key(rlk)
+        self._ck(self.lib.fhe_mul_relin(self.h, _ptr(a), _ptr(b), _ptr(rlk), _ptr(out), n), "fhe_mul_relin")
         return out
 
     def keyswitch(self, d, ksk, out):
-        self._ck(self.lib.fhe_keyswitch(self.h, _ptr(d), _ptr(ksk), _ptr(out), d.shape[0]), "fhe_keyswitch")
+        n = self._ct_batch(out)
+        if tuple(d.shape) != (n, self.L, self.n):
+            raise FheBackendError(f"keyswitch input shape {tuple(d.shape)}, expected {(n, self.L, self.n)}")
+        self._on_device(d)
+        self._key(ksk)
+        self._ck(self.lib.fhe_keyswitch(self.h, _ptr(d), _ptr(ksk), _ptr(out), n), "fhe_keyswitch")
         return out
 
     def rotate(self, ct, galois: int, gk, out):
-        self._ck(self.lib.fhe_rotate(self.h, _ptr(ct), galois, _ptr(gk), _ptr(out), ct.shape[0]), "fhe_rotate")
+        n = self._ct_batch(ct, out)
+        self._key(gk)
+        self._ck(self.lib.fhe_rotate(self.h, _ptr(ct), galois, _ptr(gk), _ptr(out), n), "fhe_rotate")
         return out
 
     def reduce(self, cts, op: int, rlk=None, out=None):
         """Balanced-tree reduction of cts [n][2][L][N] to out [1][2][L][N] (cts is scratch)."""
         out = cts[:1] if out is None else out
+        self._ct_batch(cts)
+        if out.dim() != 4 or out.shape[0] < 1:
+            raise FheBackendError("reduce output must hold one ciphertext")
+        self._ct_batch(out)
+        if rlk is not None:
+            self._key(rlk)
         self._ck(self.lib.fhe_reduce(self.h, _ptr(cts), cts.shape[0], op, _ptr(rlk) if rlk is not None else None,
                                      _ptr(out)), "fhe_reduce")
         return out
@@ -249,6 +295,7 @@ class Context:
         return g.value
 
     def bcast_key(self, key, nccl_comm: int, root: int = 0):
+        self._on_device(key)
         self._ck(self.lib.fhe_bcast_key(self.h, _ptr(key), key.numel(), nccl_comm, root), "fhe_bcast_key")
 
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <string>
 #include <vector>
 
@@ -73,9 +74,28 @@ struct fhe_ctx {
   ConvTab moddown{};           // P -> Q, h scaled by R
   std::vector<void *> blobs;   // device allocations owned by the context
   void *behz = nullptr;        // BEHZ device constants (BFV)
+  // fhe_base_conv tables by (src ids, ~0, dst ids); their device arrays are
+  // blobs of this context, so they are freed with it
+  std::map<std::vector<u32>, ConvTab> conv_cache;
   // scratch
   void *ws = nullptr;
   size_t ws_bytes = 0;
+};
+
+// Binds the context's device for the duration of an ABI call and restores the
+// caller's current device: a host thread may drive contexts on several GPUs,
+// and workspace allocations / null-stream launches follow the current device.
+struct DeviceBind {
+  int prev = -1;
+  explicit DeviceBind(const fhe_ctx *c) {
+    if (c && hipGetDevice(&prev) == hipSuccess && prev != c->device) (void)hipSetDevice(c->device);
+    else prev = -1;
+  }
+  ~DeviceBind() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceBind(const DeviceBind &) = delete;
+  DeviceBind &operator=(const DeviceBind &) = delete;
 };
 
 // helpers shared by the translation units (fhe_backend.cpp)

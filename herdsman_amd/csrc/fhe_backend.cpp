@@ -164,6 +164,7 @@ static void ctx_release(fhe_ctx *c) {
   if (!c) return;
   for (void *p : c->blobs) (void)hipFree(p);
   c->blobs.clear();
+  c->conv_cache.clear();
   if (c->ws) (void)hipFree(c->ws);
   c->ws = nullptr;
 }
@@ -325,11 +326,13 @@ int fhe_set_stream(fhe_ctx *c, void *stream) {
 
 int fhe_synchronize(fhe_ctx *c) {
   if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
   return fhe_check(c, hipStreamSynchronize(c->stream), "synchronize");
 }
 
 int fhe_reserve(fhe_ctx *c, uint32_t max_batch) {
   if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
   max_batch = std::min(max_batch, kCtChunk);  // ops run in passes of at most kCtChunk ciphertexts
   size_t need = (size_t)sizeof(u64) * c->n * max_batch * 2 * c->L;  // rotate / mul scratch
   if (c->K) need += keyswitch_ws_bytes(c, max_batch);
@@ -340,14 +343,17 @@ int fhe_reserve(fhe_ctx *c, uint32_t max_batch) {
 
 int fhe_dev_alloc(fhe_ctx *c, size_t bytes, void **out) {
   if (!c || !out) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
   return fhe_check(c, hipMalloc(out, bytes), "hipMalloc");
 }
 int fhe_dev_free(fhe_ctx *c, void *ptr) {
   if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
   return fhe_check(c, hipFree(ptr), "hipFree");
 }
 int fhe_memcpy_h2d(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
   if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
   int rc = fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream), "h2d");
   if (rc) return rc;
   // the host buffer may be reused as soon as this returns (callers stage
@@ -356,6 +362,7 @@ int fhe_memcpy_h2d(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
 }
 int fhe_memcpy_d2h(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
   if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
   int rc = fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream), "d2h");
   if (rc) return rc;
   return fhe_check(c, hipStreamSynchronize(c->stream), "d2h sync");
@@ -372,11 +379,13 @@ static int check_range(fhe_ctx *c, const void *p, uint32_t mod_begin, uint32_t n
 int fhe_ntt_fwd(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs) {
   int rc = check_range(c, data, mod_begin, n_limbs, n_polys);
   if (rc) return rc;
+  DeviceBind bind(c);
   return ntt_launch(c, LimbMap{data, n_limbs, n_limbs, 0, n_limbs, 0, mod_begin, n_polys}, false);
 }
 int fhe_ntt_inv(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs) {
   int rc = check_range(c, data, mod_begin, n_limbs, n_polys);
   if (rc) return rc;
+  DeviceBind bind(c);
   return ntt_launch(c, LimbMap{data, n_limbs, n_limbs, 0, n_limbs, 0, mod_begin, n_polys}, true);
 }
 
@@ -384,6 +393,7 @@ static int ew(fhe_ctx *c, EwOp op, const uint64_t *a, const uint64_t *b, uint64_
               uint32_t mod_begin, uint32_t n_limbs) {
   int rc = check_range(c, a, mod_begin, n_limbs, n_polys);
   if (rc) return rc;
+  DeviceBind bind(c);
   if (!n_polys) return FHE_OK;
   if (!b || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   return ew_launch(c, op, a, b, out, n_polys, mod_begin, n_limbs);
@@ -408,16 +418,16 @@ int fhe_base_conv(fhe_ctx *c, const uint64_t *src, const uint32_t *src_mods, uin
     if (x >= c->nmod) return fhe_fail(c, FHE_ERR_INVALID, "modulus id");
   for (u32 x : d)
     if (x >= c->nmod) return fhe_fail(c, FHE_ERR_INVALID, "modulus id");
-  static thread_local std::map<std::pair<const fhe_ctx *, std::vector<u32>>, ConvTab> cache;
+  DeviceBind bind(c);
   std::vector<u32> key(s);
   key.push_back(~0u);
   key.insert(key.end(), d.begin(), d.end());
-  auto it = cache.find({c, key});
+  auto it = c->conv_cache.find(key);
   ConvTab t;
-  if (it == cache.end()) {
+  if (it == c->conv_cache.end()) {
     t = make_conv_tab(c, s, d, 1);
     if (!t.h) return fhe_fail(c, FHE_ERR_OOM, "conv table");
-    cache[{c, key}] = t;
+    c->conv_cache.emplace(std::move(key), t);
   } else {
     t = it->second;
   }
@@ -428,6 +438,7 @@ int fhe_fill_uniform(fhe_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_
                      uint64_t seed) {
   int rc = check_range(c, data, mod_begin, n_limbs, n_polys);
   if (rc) return rc;
+  DeviceBind bind(c);
   return fill_uniform_launch(c, data, n_polys, mod_begin, n_limbs, seed);
 }
 
@@ -449,6 +460,7 @@ int fhe_mul_relin(fhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64
                   uint32_t n_ct) {
   int rc = need_ks(c, a, rlk, out, n_ct);
   if (rc) return rc;
+  DeviceBind bind(c);
   if (!n_ct) return FHE_OK;
   if (!b) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   const size_t cw = (size_t)2 * c->L * c->n;
@@ -465,6 +477,7 @@ int fhe_mul_relin(fhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64
 int fhe_keyswitch(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n) {
   int rc = need_ks(c, d, ksk, out, n);
   if (rc) return rc;
+  DeviceBind bind(c);
   if (!n) return FHE_OK;
   void *ws;
   if ((rc = ctx_workspace(c, keyswitch_ws_bytes(c, std::min(n, kCtChunk)), &ws))) return rc;
@@ -481,6 +494,7 @@ int fhe_keyswitch(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *
 int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out, uint32_t n_ct) {
   int rc = need_ks(c, ct, gk, out, n_ct);
   if (rc) return rc;
+  DeviceBind bind(c);
   if ((g & 1) == 0 || g >= 2 * c->n) return fhe_fail(c, FHE_ERR_INVALID, "galois element must be odd and < 2N");
   if (!n_ct) return FHE_OK;
   const size_t cw = (size_t)2 * c->L * c->n;
@@ -506,6 +520,7 @@ static int combine(fhe_ctx *c, int op, uint64_t *a, const uint64_t *b, const uin
 
 int fhe_reduce(fhe_ctx *c, uint64_t *cts, uint32_t n_ct, int op, const uint64_t *rlk, uint64_t *out) {
   if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
   if (!cts || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
   if (op != FHE_REDUCE_ADD && op != FHE_REDUCE_MUL_RELIN) return fhe_fail(c, FHE_ERR_INVALID, "reduce op");
   if (op == FHE_REDUCE_MUL_RELIN && !rlk) return fhe_fail(c, FHE_ERR_INVALID, "reduce MUL_RELIN needs rlk");
@@ -541,6 +556,7 @@ int fhe_reduce_schedule(int rank, int world, int root, int32_t *steps, int cap) 
 
 int fhe_reduce_ranks(fhe_ctx *c, uint64_t *ct, int op, const uint64_t *rlk, void *comm, int root, uint64_t *tmp) {
   if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
   if (!ct || !comm || !tmp) return fhe_fail(c, FHE_ERR_INVALID, "null argument");
   if (op != FHE_REDUCE_ADD && op != FHE_REDUCE_MUL_RELIN) return fhe_fail(c, FHE_ERR_INVALID, "reduce op");
   if (op == FHE_REDUCE_MUL_RELIN && !rlk) return fhe_fail(c, FHE_ERR_INVALID, "reduce MUL_RELIN needs rlk");
@@ -568,6 +584,7 @@ int fhe_reduce_ranks(fhe_ctx *c, uint64_t *ct, int op, const uint64_t *rlk, void
 
 int fhe_bcast_key(fhe_ctx *c, uint64_t *key, size_t words, void *comm, int root) {
   if (!c || !key || !comm) return fhe_fail(c, FHE_ERR_INVALID, "null argument");
+  DeviceBind bind(c);
   ncclResult_t r = ncclBroadcast(key, key, words, ncclUint64, root, (ncclComm_t)comm, c->stream);
   if (r != ncclSuccess) return fhe_fail(c, FHE_ERR_DEVICE, std::string("ncclBroadcast: ") + ncclGetErrorString(r));
   return FHE_OK;

@@ -10,6 +10,7 @@ import re
 import subprocess
 
 import pytest
+import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "plugins", "fhe_backend.h")
@@ -80,3 +81,39 @@ def test_reduce_schedule_c_matches_python(lib):
                 assert hb.reduce_schedule(rank, world, root) == reduce_schedule(rank, world, root)
     with pytest.raises(hb.FheBackendError):
         hb.reduce_schedule(2, 2, 0)
+
+
+def _bare_context(hb, log_n=12, L=3, K=2, dnum=2):
+    """A Context with its parameters but no device handle: the argument checks
+    run before anything crosses the ABI, so they are testable without a GPU."""
+    c = hb.Context.__new__(hb.Context)
+    c.lib, c.h = None, None
+    c.scheme, c.log_n, c.n, c.L, c.K, c.dnum = 0, log_n, 1 << log_n, L, K, dnum
+    c.moduli = np.zeros(L + K, dtype=np.uint64)
+    c.device = 0
+    return c
+
+
+def test_binding_rejects_bad_shapes_and_devices():
+    """a short output, a wrong key or a tensor on another device must be
+    rejected in the binding, never handed to the kernels as a raw pointer."""
+    import torch
+    import herdsman_amd.backend as hb
+
+    c = _bare_context(hb)
+    ct = lambda n: torch.empty((n, 2, 3, 1 << 12), dtype=torch.int64)
+    key = torch.empty((2, 2, 5, 1 << 12), dtype=torch.int64)
+    bad = [
+        lambda: c.mul_relin(ct(2), ct(2), key, ct(1)),                      # short output
+        lambda: c.mul_relin(ct(2), ct(3), key, ct(2)),                      # operand batch mismatch
+        lambda: c.mul_relin(ct(2), ct(2), key[:1], ct(2)),                  # wrong key
+        lambda: c.rotate(ct(2), 5, torch.empty((2, 2, 3, 1 << 12), dtype=torch.int64), ct(2)),
+        lambda: c.add(ct(1), ct(1), torch.empty((1, 2, 3, 1 << 11), dtype=torch.int64)),
+        lambda: c.keyswitch(torch.empty((2, 2, 1 << 12), dtype=torch.int64), key, ct(2)),
+        lambda: c.ntt_fwd(torch.empty((1, 3, 1 << 12), dtype=torch.int64), mod_begin=3),  # limbs past the moduli
+        lambda: c.reduce(ct(3), hb.REDUCE_ADD, out=torch.empty((2, 3, 1 << 12), dtype=torch.int64)),
+        lambda: c.mul_relin(ct(2), ct(2), key, ct(2)),                      # right shapes, host tensors
+    ]
+    for i, f in enumerate(bad):
+        with pytest.raises(hb.FheBackendError):
+            f()

@@ -631,3 +631,24 @@ def test_concurrent_contexts_on_streams(hb):
             c.mul_relin(da[sl], db[sl], dk, dout[sl])
     torch.cuda.synchronize()
     assert np.array_equal(hb.to_host(dout), o.mul_relin(a, b, k))
+
+
+def test_base_conv_contexts_recreated(hb):
+    """fhe_base_conv's tables belong to the context.  Contexts with
+    different moduli / ring sizes are created, used and destroyed in sequence
+    (a freed context's address is typically handed to the next one) with the
+    same index lists; every conversion must match the oracle of ITS context."""
+    import torch
+
+    src, dst = [0, 1, 2], [3, 4, 5, 6]
+    for rep, (log_n, bits) in enumerate([(12, 60), (12, 55), (13, 60), (12, 50)]):
+        mods = np.array(_generic_primes(bits, log_n, 7), dtype=np.uint64) if bits != 60 else None
+        o = Oracle(SCHEME_CKKS, log_n, 7, moduli=mods)
+        c = hb.Context(SCHEME_CKKS, log_n, 7, moduli=o.moduli)
+        x = o.uniform((2, 3, 1 << log_n), seed=190 + rep)
+        y = hb.empty((2, len(dst), 1 << log_n))
+        c.base_conv(hb.to_device(x), src, y, dst)
+        c.base_conv(hb.to_device(x), src, y, dst)  # cached table
+        torch.cuda.synchronize()
+        assert np.array_equal(hb.to_host(y), o.base_conv(x, src, dst)), (log_n, bits)
+        c.close()
