@@ -57,6 +57,11 @@ SIGNATURES = {
     "fhe_dev_free": (C.c_int, [_vp, _vp]),
     "fhe_memcpy_h2d": (C.c_int, [_vp, _vp, _vp, _sz]),
     "fhe_memcpy_d2h": (C.c_int, [_vp, _vp, _vp, _sz]),
+    "fhe_host_alloc": (C.c_int, [_vp, _sz, C.POINTER(_vp)]),
+    "fhe_host_free": (C.c_int, [_vp, _vp]),
+    "fhe_memcpy_h2d_async": (C.c_int, [_vp, _vp, _vp, _sz]),
+    "fhe_memcpy_d2h_async": (C.c_int, [_vp, _vp, _vp, _sz]),
+    "fhe_use_own_stream": (C.c_int, [_vp]),
     "fhe_ntt_fwd": (C.c_int, [_vp, _vp, _u32, _u32, _u32]),
     "fhe_ntt_inv": (C.c_int, [_vp, _vp, _u32, _u32, _u32]),
     "fhe_poly_add": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32, _u32]),

@@ -55,6 +55,7 @@ struct fhe_ctx {
   fhe_params params{};
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;  // fhe_use_own_stream
   std::string err;
   u32 log_n = 0, n = 0, L = 0, K = 0, dnum = 0, alpha = 0, nB = 0, nmod = 0;
   u64 t = 0;

@@ -167,6 +167,8 @@ static void ctx_release(fhe_ctx *c) {
   c->conv_cache.clear();
   if (c->ws) (void)hipFree(c->ws);
   c->ws = nullptr;
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  c->own_stream = nullptr;
 }
 
 // ------------------------------------------------------------ context
@@ -366,6 +368,36 @@ int fhe_memcpy_d2h(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
   int rc = fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream), "d2h");
   if (rc) return rc;
   return fhe_check(c, hipStreamSynchronize(c->stream), "d2h sync");
+}
+
+int fhe_host_alloc(fhe_ctx *c, size_t bytes, void **out) {
+  if (!c || !out) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
+  return fhe_check(c, hipHostMalloc(out, bytes, hipHostMallocDefault), "hipHostMalloc");
+}
+int fhe_host_free(fhe_ctx *c, void *ptr) {
+  if (!c) return FHE_ERR_INVALID;
+  return fhe_check(c, hipHostFree(ptr), "hipHostFree");
+}
+int fhe_memcpy_h2d_async(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
+  return fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream), "h2d async");
+}
+int fhe_memcpy_d2h_async(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
+  return fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream), "d2h async");
+}
+int fhe_use_own_stream(fhe_ctx *c) {
+  if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
+  if (!c->own_stream) {
+    int rc = fhe_check(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream create");
+    if (rc) return rc;
+  }
+  c->stream = c->own_stream;
+  return FHE_OK;
 }
 
 // an empty batch (count == 0) is a no-op that accepts null buffers

@@ -1,6 +1,7 @@
 // gpu_worker_group.cpp -- see gpu_worker_group.hpp.
 #include "gpu_worker_group.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <fstream>
@@ -98,26 +99,127 @@ struct KeySet {
   std::map<uint32_t, DevBuf> galois;
 };
 
+// Device buffers of one lane, recycled across instructions and batches: a
+// buffer handed back is reused by a later op on the SAME stream, which stream
+// order makes safe, so the steady state does no hipMalloc / hipFree.
+class Arena {
+ public:
+  explicit Arena(fhe_ctx *c) : ctx_(c) {}
+  Arena(const Arena &) = delete;
+  Arena &operator=(const Arena &) = delete;
+  ~Arena() {
+    for (auto &b : free_) fhe_dev_free(ctx_, b.second);
+  }
+  uint64_t *get(size_t words, size_t *cap) {
+    auto it = free_.lower_bound(words);  // best fit
+    if (it != free_.end()) {
+      *cap = it->first;
+      uint64_t *p = it->second;
+      free_.erase(it);
+      return p;
+    }
+    void *q = nullptr;
+    ck(ctx_, fhe_dev_alloc(ctx_, words * 8, &q), "arena alloc");
+    *cap = words;
+    return static_cast<uint64_t *>(q);
+  }
+  void put(uint64_t *p, size_t cap) { free_.emplace(cap, p); }
+
+ private:
+  fhe_ctx *ctx_;
+  std::multimap<size_t, uint64_t *> free_;
+};
+
+struct ArenaBuf {
+  Arena *arena = nullptr;
+  uint64_t *p = nullptr;
+  size_t cap = 0;
+  ArenaBuf() = default;
+  ArenaBuf(Arena &a, size_t words) : arena(&a) { p = a.get(words, &cap); }
+  ArenaBuf(const ArenaBuf &) = delete;
+  ArenaBuf &operator=(const ArenaBuf &) = delete;
+  ArenaBuf(ArenaBuf &&o) noexcept { *this = std::move(o); }
+  ArenaBuf &operator=(ArenaBuf &&o) noexcept {
+    std::swap(arena, o.arena);
+    std::swap(p, o.p);
+    std::swap(cap, o.cap);
+    return *this;
+  }
+  ~ArenaBuf() {
+    if (p) arena->put(p, cap);
+  }
+};
+
+// Pinned host staging buffer (fhe_host_alloc), grown on demand.
+struct Pinned {
+  fhe_ctx *ctx = nullptr;
+  uint8_t *p = nullptr;
+  size_t bytes = 0;
+  Pinned() = default;
+  Pinned(const Pinned &) = delete;
+  Pinned &operator=(const Pinned &) = delete;
+  ~Pinned() {
+    if (p) fhe_host_free(ctx, p);
+  }
+  uint8_t *reserve(fhe_ctx *c, size_t need) {
+    if (need > bytes) {
+      if (p) fhe_host_free(ctx, p);
+      p = nullptr;
+      bytes = 0;
+      void *q = nullptr;
+      ck(c, fhe_host_alloc(c, need, &q), "pinned host alloc");
+      ctx = c;
+      p = static_cast<uint8_t *>(q);
+      bytes = need;
+    }
+    return p;
+  }
+};
+
+// one lane's state for one schema: context (own stream), buffers, staging
+struct LaneSchema {
+  SchemaCtx s;
+  std::unique_ptr<Arena> arena;
+  std::vector<std::unique_ptr<Pinned>> in_stage;  // one per PUSH_INPUT of a batch
+  Pinned out_stage;
+};
+
 }  // namespace
+
+struct GpuWorkerGroup::Job {
+  std::shared_ptr<Handle> handle;
+  herd::common::task_t task;
+};
+
+struct GpuWorkerGroup::Lane {
+  std::thread thread;
+  std::map<int, std::unique_ptr<LaneSchema>> schemas;  // schema -> this lane's context
+};
 
 struct GpuWorkerGroup::Device {
   int id = 0;
-  std::thread thread;
   std::mutex m;
   std::condition_variable cv;
   std::deque<Job> queue;
-  std::map<int, SchemaCtx> ctx;                                 // schema -> context
-  std::map<std::pair<std::string, int>, std::shared_ptr<KeySet>> keys;  // (session, schema)
+  bool stop = false;
+  std::vector<std::unique_ptr<Lane>> lanes;
+  // evaluation keys, shared by the device's lanes: (session, schema) -> keys
+  std::mutex keys_m;
+  std::map<std::pair<std::string, int>, std::shared_ptr<KeySet>> keys;
 };
 
 GpuWorkerGroup::GpuWorkerGroup(GpuWorkerGroupConfig config) : config_(std::move(config)) {
   if (config_.devices.empty()) throw std::invalid_argument("GpuWorkerGroup needs at least one device");
+  if (config_.lanes_per_device == 0) config_.lanes_per_device = 1;
+  if (config_.max_batch == 0) config_.max_batch = 1;
   for (int d : config_.devices) {
     auto dev = std::make_unique<Device>();
     dev->id = d;
+    for (uint32_t l = 0; l < config_.lanes_per_device; ++l) dev->lanes.push_back(std::make_unique<Lane>());
     devices_.push_back(std::move(dev));
   }
-  for (auto &d : devices_) d->thread = std::thread([this, p = d.get()] { device_loop(*p); });
+  for (auto &d : devices_)
+    for (auto &l : d->lanes) l->thread = std::thread([this, dp = d.get(), lp = l.get()] { lane_loop(*dp, *lp); });
   completion_thread_ = std::thread([this] { completion_loop(); });
 }
 
@@ -125,11 +227,28 @@ GpuWorkerGroup::~GpuWorkerGroup() {
   for (auto &d : devices_) {
     {
       std::lock_guard lk(d->m);
-      d->queue.push_back(Job{nullptr, {}});  // stop marker
+      d->stop = true;
     }
-    d->cv.notify_one();
+    d->cv.notify_all();
   }
-  for (auto &d : devices_) d->thread.join();
+  for (auto &d : devices_)
+    for (auto &l : d->lanes) l->thread.join();
+  // teardown order: keys and lane buffers are freed through their contexts,
+  // so they go before the contexts
+  for (auto &d : devices_) {
+    d->keys.clear();
+    for (auto &l : d->lanes) {
+      for (auto &kv : l->schemas) {
+        LaneSchema &ls = *kv.second;
+        ls.arena.reset();
+        ls.in_stage.clear();
+        if (ls.out_stage.p) fhe_host_free(ls.out_stage.ctx, ls.out_stage.p);
+        ls.out_stage.p = nullptr;
+        fhe_ctx_destroy(ls.s.ctx);
+      }
+      l->schemas.clear();
+    }
+  }
   {
     std::lock_guard lk(done_mutex_);
     stopping_ = true;
@@ -139,7 +258,7 @@ GpuWorkerGroup::~GpuWorkerGroup() {
 }
 
 std::size_t GpuWorkerGroup::concurrent_workers() const noexcept {
-  return devices_.size() * config_.tasks_per_device;
+  return devices_.size() * config_.lanes_per_device;
 }
 
 std::shared_ptr<IWorkerGroup::TaskHandle> GpuWorkerGroup::schedule_task(const herd::common::task_t &task) {
@@ -168,44 +287,86 @@ void GpuWorkerGroup::complete(const std::shared_ptr<Handle> &h, Status st) {
 
 void GpuWorkerGroup::completion_loop() {
   std::vector<std::shared_ptr<Handle>> waiting;  // completed, callback not attached yet
+  // poll interval for undelivered handles: 50 us right after a completion
+  // (the executor attaches its callback within microseconds), backing off to
+  // 5 ms while nothing is delivered
+  auto poll = std::chrono::microseconds(50);
   std::unique_lock lk(done_mutex_);
   while (true) {
-    done_cv_.wait_for(lk, std::chrono::microseconds(waiting.empty() ? 100000 : 50),
+    done_cv_.wait_for(lk, waiting.empty() ? std::chrono::microseconds(100000) : poll,
                       [&] { return stopping_ || !done_.empty(); });
+    const bool fresh = !done_.empty();
     while (!done_.empty()) {
       waiting.push_back(std::move(done_.front()));
       done_.pop_front();
     }
     const bool stop = stopping_;
     lk.unlock();
+    size_t delivered = 0;
     for (size_t i = 0; i < waiting.size();) {
       if (waiting[i]->try_deliver()) {
         waiting[i] = std::move(waiting.back());
         waiting.pop_back();
+        ++delivered;
       } else {
         ++i;
       }
     }
+    poll = (fresh || delivered) ? std::chrono::microseconds(50) : std::min(poll * 2, std::chrono::microseconds(5000));
     lk.lock();
-    if (stop && done_.empty()) return;
+    if (stop && done_.empty()) return;  // handles never picked up by a callback are dropped here
   }
 }
 
 // ------------------------------------------------------------- evaluation
 namespace {
 
-SchemaCtx &schema_ctx(std::map<int, SchemaCtx> &m, const GpuWorkerGroupConfig &cfg, int device, int schema) {
+enum class Op : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4 };
+struct Instr {
+  Op op;
+  int32_t arg;
+};
+
+// herd_common's Circuit -> the backend's stack program.  The stand-in circuit
+// (herd_common_standin.hpp) IS such a program; a herd_common Circuit with
+// another shape compiles and fails its tasks loudly until its gates are
+// mapped here (circuit interpretation, SURVEY.md §8f-4, is blocked on the
+// absent herd_common).
+template <class C>
+std::vector<Instr> lower_circuit(const C &c) {
+  if constexpr (requires { c.program.begin()->op; c.program.begin()->arg; }) {
+    std::vector<Instr> out;
+    for (const auto &i : c.program) {
+      const uint32_t op = static_cast<uint32_t>(i.op);
+      if (op > static_cast<uint32_t>(Op::ROTATE)) throw std::runtime_error("unknown circuit op");
+      out.push_back(Instr{static_cast<Op>(op), static_cast<int32_t>(i.arg)});
+    }
+    return out;
+  } else {
+    throw std::runtime_error("no lowering from this herd_common Circuit to backend ops (INTEGRATION.md §2)");
+  }
+}
+
+template <class T>
+int schema_id(T v) {
+  return static_cast<int>(v);  // herd_common's SchemaType is an enum (key_service.cpp:28)
+}
+
+LaneSchema &lane_schema(std::map<int, std::unique_ptr<LaneSchema>> &m, const GpuWorkerGroupConfig &cfg, int device,
+                        int schema) {
   auto it = m.find(schema);
-  if (it != m.end()) return it->second;
+  if (it != m.end()) return *it->second;
   const SchemaParams *sp = nullptr;
   for (const auto &s : cfg.schemas)
     if (s.schema_type == schema) sp = &s;
   if (!sp) throw std::runtime_error("no backend parameters for schema " + std::to_string(schema));
   fhe_params p = sp->params;
   p.moduli = sp->moduli.empty() ? nullptr : sp->moduli.data();
-  SchemaCtx s;
+  auto ls = std::make_unique<LaneSchema>();
+  SchemaCtx &s = ls->s;
   if (fhe_ctx_create(&p, device, &s.ctx) != FHE_OK)
     throw std::runtime_error(std::string("fhe_ctx_create: ") + fhe_last_error(nullptr));
+  ls->arena = std::make_unique<Arena>(s.ctx);
   s.scheme = p.scheme;
   s.log_n = p.log_n;
   s.L = p.num_q;
@@ -217,7 +378,11 @@ SchemaCtx &schema_ctx(std::map<int, SchemaCtx> &m, const GpuWorkerGroupConfig &c
   fhe_ctx_moduli(s.ctx, s.moduli.data(), cnt, nullptr);
   s.q_digest = moduli_digest(s.moduli.data(), s.L);
   s.qp_digest = moduli_digest(s.moduli.data(), s.L + s.K);
-  return m.emplace(schema, s).first->second;
+  auto &slot = m[schema];
+  slot = std::move(ls);
+  // the lane's own stream: lanes of one device run concurrently
+  ck(slot->s.ctx, fhe_use_own_stream(slot->s.ctx), "own stream");
+  return *slot;
 }
 
 std::shared_ptr<KeySet> load_keys(const SchemaCtx &s, const std::filesystem::path &file) {
@@ -241,8 +406,18 @@ std::shared_ptr<KeySet> load_keys(const SchemaCtx &s, const std::filesystem::pat
     if (e.kind == 0) ks->relin = std::move(d);
     else ks->galois.emplace(e.galois_elt, std::move(d));
   }
-  ck(s.ctx, fhe_synchronize(s.ctx), "key upload sync");
+  ck(s.ctx, fhe_synchronize(s.ctx), "key upload sync");  // visible to every lane's stream from here on
   return ks;
+}
+
+// the device's keys for (session, schema), loaded once through the asking lane
+std::shared_ptr<KeySet> device_keys(std::mutex &m, std::map<std::pair<std::string, int>, std::shared_ptr<KeySet>> &keys,
+                                    const SchemaCtx &s, const std::filesystem::path &key_dir,
+                                    const std::string &session, int schema) {
+  std::lock_guard lk(m);
+  auto &k = keys[std::make_pair(session, schema)];
+  if (!k) k = load_keys(s, key_dir / session / (std::to_string(schema) + ".key"));
+  return k;
 }
 
 // parse ciphertext k of a row
@@ -277,33 +452,39 @@ const DevBuf &galois_key(const SchemaCtx &s, const KeySet &ks, int32_t steps, ui
   return it->second;
 }
 
-// evaluate the circuit program on `n` rows at once; rows[r] ciphertexts are the inputs
-void eval_map_batch(const SchemaCtx &s, const KeySet &ks, const herd::common::Circuit &circ,
+// Evaluate the program on `n` rows at once.  Every input is staged into its
+// own pinned buffer and copied asynchronously, so the host gathers input k+1
+// while input k is on the wire and earlier kernels run; the batch ends with
+// one asynchronous copy back and one synchronisation.
+void eval_map_batch(LaneSchema &ls, const KeySet &ks, const std::vector<Instr> &prog,
                     const std::vector<std::vector<uint8_t>> &rows, size_t r0, size_t n,
                     std::vector<std::vector<uint8_t>> &out_rows) {
+  const SchemaCtx &s = ls.s;
   const size_t cw = s.ct_words();
-  std::vector<DevBuf> stack;
-  std::vector<uint64_t> host(cw * n);
-  for (const auto &ins : circ.program) {
+  std::vector<ArenaBuf> stack;
+  size_t push = 0;
+  for (const auto &ins : prog) {
     switch (ins.op) {
-      case herd::common::CtOp::PUSH_INPUT: {
-        for (size_t r = 0; r < n; ++r) std::memcpy(host.data() + r * cw, row_ct(s, rows[r0 + r], ins.arg), cw * 8);
-        DevBuf d(s.ctx, cw * n);
-        ck(s.ctx, fhe_memcpy_h2d(s.ctx, d.p, host.data(), cw * n * 8), "h2d");
+      case Op::PUSH_INPUT: {
+        if (ls.in_stage.size() <= push) ls.in_stage.push_back(std::make_unique<Pinned>());
+        uint64_t *host = reinterpret_cast<uint64_t *>(ls.in_stage[push++]->reserve(s.ctx, cw * n * 8));
+        for (size_t r = 0; r < n; ++r) std::memcpy(host + r * cw, row_ct(s, rows[r0 + r], ins.arg), cw * 8);
+        ArenaBuf d(*ls.arena, cw * n);
+        ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, d.p, host, cw * n * 8), "h2d");
         stack.push_back(std::move(d));
         break;
       }
-      case herd::common::CtOp::ADD:
-      case herd::common::CtOp::SUB:
-      case herd::common::CtOp::MUL_RELIN: {
+      case Op::ADD:
+      case Op::SUB:
+      case Op::MUL_RELIN: {
         if (stack.size() < 2) throw std::runtime_error("circuit stack underflow");
-        DevBuf b = std::move(stack.back());
+        ArenaBuf b = std::move(stack.back());
         stack.pop_back();
-        DevBuf a = std::move(stack.back());
+        ArenaBuf a = std::move(stack.back());
         stack.pop_back();
-        DevBuf o(s.ctx, cw * n);
-        if (ins.op == herd::common::CtOp::ADD) ck(s.ctx, fhe_add(s.ctx, a.p, b.p, o.p, (uint32_t)n), "add");
-        else if (ins.op == herd::common::CtOp::SUB) ck(s.ctx, fhe_sub(s.ctx, a.p, b.p, o.p, (uint32_t)n), "sub");
+        ArenaBuf o(*ls.arena, cw * n);
+        if (ins.op == Op::ADD) ck(s.ctx, fhe_add(s.ctx, a.p, b.p, o.p, (uint32_t)n), "add");
+        else if (ins.op == Op::SUB) ck(s.ctx, fhe_sub(s.ctx, a.p, b.p, o.p, (uint32_t)n), "sub");
         else {
           if (!ks.relin.p) throw std::runtime_error("no relinearisation key");
           ck(s.ctx, fhe_mul_relin(s.ctx, a.p, b.p, ks.relin.p, o.p, (uint32_t)n), "mul_relin");
@@ -311,11 +492,11 @@ void eval_map_batch(const SchemaCtx &s, const KeySet &ks, const herd::common::Ci
         stack.push_back(std::move(o));
         break;
       }
-      case herd::common::CtOp::ROTATE: {
+      case Op::ROTATE: {
         if (stack.empty()) throw std::runtime_error("circuit stack underflow");
         uint32_t g = 0;
         const DevBuf &gk = galois_key(s, ks, ins.arg, &g);
-        DevBuf o(s.ctx, cw * n);
+        ArenaBuf o(*ls.arena, cw * n);
         ck(s.ctx, fhe_rotate(s.ctx, stack.back().p, g, gk.p, o.p, (uint32_t)n), "rotate");
         stack.back() = std::move(o);
         break;
@@ -325,8 +506,10 @@ void eval_map_batch(const SchemaCtx &s, const KeySet &ks, const herd::common::Ci
     }
   }
   if (stack.size() != 1) throw std::runtime_error("circuit must leave exactly one ciphertext");
-  ck(s.ctx, fhe_memcpy_d2h(s.ctx, host.data(), stack.back().p, cw * n * 8), "d2h");
-  for (size_t r = 0; r < n; ++r) out_rows.push_back(make_row(s, host.data() + r * cw));
+  uint64_t *host = reinterpret_cast<uint64_t *>(ls.out_stage.reserve(s.ctx, cw * n * 8));
+  ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, host, stack.back().p, cw * n * 8), "d2h");
+  ck(s.ctx, fhe_synchronize(s.ctx), "batch sync");  // staging buffers are free again after this
+  for (size_t r = 0; r < n; ++r) out_rows.push_back(make_row(s, host + r * cw));
 }
 
 std::filesystem::path frame_path(const std::filesystem::path &root, const herd::common::UUID &session,
@@ -336,32 +519,30 @@ std::filesystem::path frame_path(const std::filesystem::path &root, const herd::
 
 }  // namespace
 
-void GpuWorkerGroup::device_loop(Device &dev) {
+void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
   while (true) {
     Job job;
     {
       std::unique_lock lk(dev.m);
-      dev.cv.wait(lk, [&] { return !dev.queue.empty(); });
+      dev.cv.wait(lk, [&] { return dev.stop || !dev.queue.empty(); });
+      if (dev.queue.empty()) break;  // stopping and drained
       job = std::move(dev.queue.front());
       dev.queue.pop_front();
     }
-    if (!job.handle) break;
     Status st = Status::COMPLETED;
     try {
       if (std::holds_alternative<herd::common::MapTask>(job.task)) {
         const auto &t = std::get<herd::common::MapTask>(job.task);
-        SchemaCtx &s = schema_ctx(dev.ctx, config_, dev.id, t.crypto_key_ptr.schema_type);
-        auto key_id = std::make_pair(t.session_uuid.as_string(), t.crypto_key_ptr.schema_type);
-        auto &ks = dev.keys[key_id];
-        if (!ks)
-          ks = load_keys(s, config_.key_dir / t.session_uuid.as_string() /
-                                (std::to_string(t.crypto_key_ptr.schema_type) + ".key"));
+        const int schema = schema_id(t.crypto_key_ptr.schema_type);
+        const std::vector<Instr> prog = lower_circuit(t.circuit);
+        LaneSchema &ls = lane_schema(lane.schemas, config_, dev.id, schema);
+        auto ks = device_keys(dev.keys_m, dev.keys, ls.s, config_.key_dir, t.session_uuid.as_string(), schema);
         const auto rows = read_partition(frame_path(config_.storage_dir, t.session_uuid, t.input_data_frame_ptr.pointer));
         std::vector<std::vector<uint8_t>> out;
         out.reserve(rows.size());
         for (size_t r0 = 0; r0 < rows.size(); r0 += config_.max_batch) {
           const size_t n = std::min<size_t>(config_.max_batch, rows.size() - r0);
-          eval_map_batch(s, *ks, t.circuit, rows, r0, n, out);
+          eval_map_batch(ls, *ks, prog, rows, r0, n, out);
         }
         write_partition(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr), out);
       } else {
@@ -369,43 +550,37 @@ void GpuWorkerGroup::device_loop(Device &dev) {
         // ciphertext with a balanced tree of batched ADDs (MUL_RELIN if the
         // circuit's first op says so), on the GPU.
         const auto &t = std::get<herd::common::ReduceTask>(job.task);
-        SchemaCtx &s = schema_ctx(dev.ctx, config_, dev.id, t.crypto_key_ptr.schema_type);
-        const bool mul = !t.circuit.program.empty() && t.circuit.program.front().op == herd::common::CtOp::MUL_RELIN;
+        const int schema = schema_id(t.crypto_key_ptr.schema_type);
+        const std::vector<Instr> prog = lower_circuit(t.circuit);
+        LaneSchema &ls = lane_schema(lane.schemas, config_, dev.id, schema);
+        const SchemaCtx &s = ls.s;
+        const bool mul = !prog.empty() && prog.front().op == Op::MUL_RELIN;
         std::shared_ptr<KeySet> ks;
-        if (mul) {
-          auto &k = dev.keys[std::make_pair(t.session_uuid.as_string(), t.crypto_key_ptr.schema_type)];
-          if (!k)
-            k = load_keys(s, config_.key_dir / t.session_uuid.as_string() /
-                                 (std::to_string(t.crypto_key_ptr.schema_type) + ".key"));
-          ks = k;
-        }
-        std::vector<uint64_t> host;
-        size_t count = 0;
-        const size_t cw = s.ct_words();
-        for (const auto &in : t.input_data_frame_ptrs) {
-          for (const auto &row : read_partition(frame_path(config_.storage_dir, t.session_uuid, in.pointer))) {
-            host.resize((count + 1) * cw);
-            std::memcpy(host.data() + count * cw, row_ct(s, row, 0), cw * 8);
-            ++count;
-          }
-        }
-        if (count == 0) throw std::runtime_error("reduce over no rows");
-        DevBuf a(s.ctx, count * cw);
-        ck(s.ctx, fhe_memcpy_h2d(s.ctx, a.p, host.data(), count * cw * 8), "h2d");
+        if (mul) ks = device_keys(dev.keys_m, dev.keys, s, config_.key_dir, t.session_uuid.as_string(), schema);
+        std::vector<std::vector<uint8_t>> all;
+        for (const auto &in : t.input_data_frame_ptrs)
+          for (auto &row : read_partition(frame_path(config_.storage_dir, t.session_uuid, in.pointer)))
+            all.push_back(std::move(row));
+        if (all.empty()) throw std::runtime_error("reduce over no rows");
+        const size_t cw = s.ct_words(), count = all.size();
+        if (ls.in_stage.empty()) ls.in_stage.push_back(std::make_unique<Pinned>());
+        uint64_t *host = reinterpret_cast<uint64_t *>(ls.in_stage[0]->reserve(s.ctx, count * cw * 8));
+        for (size_t r = 0; r < count; ++r) std::memcpy(host + r * cw, row_ct(s, all[r], 0), cw * 8);
+        ArenaBuf a(*ls.arena, count * cw);
+        ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, a.p, host, count * cw * 8), "h2d");
         // balanced tree, one batched add / mul+relin per level (fhe_reduce)
         ck(s.ctx, fhe_reduce(s.ctx, a.p, (uint32_t)count, mul ? FHE_REDUCE_MUL_RELIN : FHE_REDUCE_ADD,
                              mul ? ks->relin.p : nullptr, a.p), "reduce");
-        std::vector<uint64_t> res(cw);
-        ck(s.ctx, fhe_memcpy_d2h(s.ctx, res.data(), a.p, cw * 8), "d2h");
-        write_partition(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr), {make_row(s, res.data())});
+        uint64_t *res = reinterpret_cast<uint64_t *>(ls.out_stage.reserve(s.ctx, cw * 8));
+        ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, res, a.p, cw * 8), "d2h");
+        ck(s.ctx, fhe_synchronize(s.ctx), "reduce sync");
+        write_partition(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr), {make_row(s, res)});
       }
     } catch (const std::exception &) {
       st = Status::ERROR;  // no exception crosses the seam (executor.cpp:168-178 fails the job)
     }
     complete(job.handle, st);
   }
-  dev.keys.clear();  // key buffers are freed through their context: before it goes
-  for (auto &kv : dev.ctx) fhe_ctx_destroy(kv.second.ctx);
 }
 
 }  // namespace herdsman_gpu

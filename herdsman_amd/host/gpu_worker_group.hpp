@@ -10,8 +10,14 @@
 //
 // Contract kept:
 //   * schedule_task never blocks on GPU work: it enqueues and returns;
-//   * one worker thread + one fhe_ctx per (device, schema) does the work,
-//     all rows of a partition in batched GPU calls;
+//   * every device runs `lanes_per_device` lanes; a lane is a host thread with
+//     its own fhe_ctx per schema and its own HIP stream, so the kernels of
+//     tasks on different lanes of one device overlap (DESIGN.md §4 "Concurrent
+//     contexts"); evaluation keys are loaded once per (session, schema) per
+//     device and shared by its lanes;
+//   * concurrent_workers() = devices x lanes_per_device: exactly the number of
+//     tasks that can be executing at once (the Executor keeps that many in
+//     flight, executor.cpp:96-113);
 //   * no exception crosses the seam: failures become Status::ERROR;
 //   * the handle stays alive in the group until its completion is delivered;
 //   * completion is delivered on the group's own completion thread, and is
@@ -20,7 +26,8 @@
 //     TaskHandle::mark_completed silently drops a completion with no callback
 //     (i_worker_group.cpp:9-12).  The handle detects delivery because the base
 //     mark_completed evaluates the virtual status() exactly when it invokes
-//     the callback.
+//     the callback.  Handles still undelivered when the group is destroyed are
+//     dropped.
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -58,8 +65,8 @@ struct GpuWorkerGroupConfig {
   std::vector<int> devices{0};
   std::filesystem::path storage_dir;  // <storage>/<session>/<frame>/<partition>
   std::filesystem::path key_dir;      // <key_dir>/<session>/<schema>.key
-  std::vector<SchemaParams> schemas;
-  uint32_t tasks_per_device = 2;      // concurrent_workers() = devices * tasks_per_device
+  std::vector<SchemaParams> schemas = default_schemas();
+  uint32_t lanes_per_device = 4;      // concurrent tasks per device (context + stream each)
   uint32_t max_batch = 64;            // rows per batched GPU call
 };
 
@@ -74,13 +81,11 @@ class GpuWorkerGroup : public IWorkerGroup {
   class Handle;
 
  private:
-  struct Job {
-    std::shared_ptr<Handle> handle;
-    herd::common::task_t task;
-  };
+  struct Job;
   struct Device;
+  struct Lane;
 
-  void device_loop(Device &dev);
+  void lane_loop(Device &dev, Lane &lane);
   void completion_loop();
   void complete(const std::shared_ptr<Handle> &h, TaskHandle::Status st);
 

@@ -6,8 +6,18 @@
 //   wg_run map    STORAGE KEYS SESSION SCHEMA PARAMS IN_FRAME PART OUT_FRAME PROGRAM...
 //   wg_run reduce STORAGE KEYS SESSION SCHEMA PARAMS OUT_FRAME OUT_PART IN_FRAME:PART... [-- mul]
 //   wg_run race   N            (seam test: N malformed tasks, callback attached late)
+//   wg_run bench  DIR PARAMS PARTS ROWS [LANES [MAX_BATCH]]
+//                 MapTask throughput: writes PARTS partitions of ROWS rows
+//                 (two ciphertexts each, uniform residues made on the GPU) and a
+//                 relinearisation key under DIR, then keeps concurrent_workers()
+//                 MapTasks "in0 in1 mul" in flight, as the Executor does
+//                 (executor.cpp:96-113), and reports ct-mult+relin/s end to end
+//                 (partition read, PCIe both ways, GPU, partition write).
 // PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file]   PROGRAM tokens: in<i> add sub mul rot:<k>
+#include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -17,6 +27,7 @@
 #include <string>
 #include <thread>
 
+#include "ct_format.hpp"
 #include "gpu_worker_group.hpp"
 
 using herdsman_gpu::GpuWorkerGroup;
@@ -82,6 +93,126 @@ static Status run(GpuWorkerGroup &g, const herd::common::task_t &task, int delay
   return f.get();
 }
 
+static void ckb(fhe_ctx *c, int rc, const char *what) {
+  if (rc != FHE_OK) throw std::runtime_error(std::string(what) + ": " + fhe_last_error(c));
+}
+
+static int bench(int argc, char **argv) {
+  if (argc < 6) throw std::runtime_error("usage: wg_run bench DIR PARAMS PARTS ROWS [LANES [MAX_BATCH]]");
+  const std::filesystem::path dir = argv[2];
+  const herdsman_gpu::SchemaParams sp = parse_params(0, argv[3]);
+  const int parts = std::atoi(argv[4]), rows = std::atoi(argv[5]);
+  GpuWorkerGroupConfig cfg;
+  cfg.storage_dir = dir / "storage";
+  cfg.key_dir = dir / "keys";
+  cfg.schemas = {sp};
+  if (argc > 6) cfg.lanes_per_device = (uint32_t)std::atoi(argv[6]);
+  if (argc > 7) cfg.max_batch = (uint32_t)std::atoi(argv[7]);
+  if (const char *d = std::getenv("WG_DEVICE")) cfg.devices = {std::atoi(d)};
+  // ---- synthetic inputs, made on the device with the backend's uniform fill
+  fhe_params p = sp.params;
+  p.moduli = sp.moduli.empty() ? nullptr : sp.moduli.data();
+  fhe_ctx *c = nullptr;
+  if (fhe_ctx_create(&p, cfg.devices[0], &c) != FHE_OK) throw std::runtime_error(fhe_last_error(nullptr));
+  uint32_t nm = 0;
+  fhe_ctx_moduli(c, nullptr, 0, &nm);
+  std::vector<uint64_t> mods(nm);
+  fhe_ctx_moduli(c, mods.data(), nm, nullptr);
+  const uint32_t L = p.num_q, K = p.num_p, dnum = p.dnum;
+  const size_t n = (size_t)1 << p.log_n, cw = 2 * L * n, kw = (size_t)dnum * 2 * (L + K) * n;
+  void *dbuf = nullptr;
+  ckb(c, fhe_dev_alloc(c, std::max(2 * cw, kw) * 8, &dbuf), "alloc");
+  std::vector<uint64_t> host(std::max(2 * cw, kw));
+  ckb(c, fhe_fill_uniform(c, (uint64_t *)dbuf, dnum * 2, 0, L + K, 0x524C4B), "fill key");
+  ckb(c, fhe_memcpy_d2h(c, host.data(), dbuf, kw * 8), "d2h");
+  {
+    std::filesystem::create_directories(cfg.key_dir / "bench");
+    std::ofstream kf(cfg.key_dir / "bench" / "0.key", std::ios::binary);
+    herdsman_gpu::KeyFileHeader h;
+    h.scheme = (uint8_t)p.scheme;
+    h.log_n = p.log_n;
+    h.L = L;
+    h.K = K;
+    h.dnum = dnum;
+    h.n_keys = 1;
+    h.moduli_digest = herdsman_gpu::moduli_digest(mods.data(), L + K);
+    herdsman_gpu::KeyEntryHeader e;
+    kf.write((const char *)&h, sizeof(h));
+    kf.write((const char *)&e, sizeof(e));
+    kf.write((const char *)host.data(), kw * 8);
+  }
+  herdsman_gpu::CtHeader ch;
+  ch.scheme = (uint8_t)p.scheme;
+  ch.domain = p.scheme == FHE_SCHEME_CKKS ? 1 : 0;
+  ch.log_n = p.log_n;
+  ch.n_limbs = L;
+  ch.moduli_digest = herdsman_gpu::moduli_digest(mods.data(), L);
+  for (int part = 0; part < parts; ++part) {
+    std::vector<std::vector<uint8_t>> rs;
+    for (int r = 0; r < rows; ++r) {
+      ckb(c, fhe_fill_uniform(c, (uint64_t *)dbuf, 4, 0, L, 0x48455244ull + (uint64_t)part * rows + r), "fill");
+      ckb(c, fhe_memcpy_d2h(c, host.data(), dbuf, 2 * cw * 8), "d2h");
+      std::vector<uint8_t> row(2 * (sizeof(ch) + cw * 8));
+      for (int k = 0; k < 2; ++k) {
+        std::memcpy(row.data() + k * (sizeof(ch) + cw * 8), &ch, sizeof(ch));
+        std::memcpy(row.data() + k * (sizeof(ch) + cw * 8) + sizeof(ch), host.data() + k * cw, cw * 8);
+      }
+      rs.push_back(std::move(row));
+    }
+    herdsman_gpu::write_partition(cfg.storage_dir / "bench" / "in" / std::to_string(part), rs);
+  }
+  fhe_dev_free(c, dbuf);
+  fhe_ctx_destroy(c);
+  // ---- the Executor's pattern: keep concurrent_workers() tasks in flight
+  herd::common::Circuit circ;
+  circ.program = {{herd::common::CtOp::PUSH_INPUT, 0}, {herd::common::CtOp::PUSH_INPUT, 1},
+                  {herd::common::CtOp::MUL_RELIN, 0}};
+  auto make = [&](int part) {
+    herd::common::MapTask t;
+    t.session_uuid = {"bench"};
+    t.input_data_frame_ptr.pointer = {{"in"}, (uint32_t)part};
+    t.input_data_frame_ptr.row_count = (uint64_t)rows;
+    t.output_data_frame_ptr = {{"out"}, (uint32_t)part};
+    t.crypto_key_ptr.schema_type = herd::common::SchemaType::CKKS;
+    t.circuit = circ;
+    return herd::common::task_t{t};
+  };
+  double best = 0;
+  for (int rep = 0; rep < 2; ++rep) {  // rep 0 warms contexts, keys and buffers
+    GpuWorkerGroup g(cfg);
+    std::mutex m;
+    std::condition_variable cv;
+    int done = 0, errors = 0, next = 0, inflight = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::unique_lock lk(m);
+    while (done < parts) {
+      while (next < parts && inflight < (int)g.concurrent_workers()) {
+        lk.unlock();
+        auto h = g.schedule_task(make(next));
+        h->set_completion_callback([&](Status s) {
+          std::lock_guard l2(m);
+          ++done;
+          --inflight;
+          if (s != Status::COMPLETED) ++errors;
+          cv.notify_one();
+        });
+        lk.lock();
+        ++next;
+        ++inflight;
+      }
+      cv.wait(lk);
+    }
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (errors) throw std::runtime_error("bench tasks failed");
+    const double rate = (double)parts * rows / dt;
+    std::printf("bench rep %d: %d MapTasks x %d rows in %.3f s = %.1f ct-mult+relin/s (%zu workers)\n", rep, parts,
+                rows, dt, rate, g.concurrent_workers());
+    best = std::max(best, rate);
+  }
+  std::printf("bench: %.1f ct-mult+relin/s\n", best);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   try {
     if (argc < 2) throw std::runtime_error("usage: wg_run map|reduce|race ...");
@@ -99,13 +230,14 @@ int main(int argc, char **argv) {
       std::printf("race: %d/%d delivered, concurrent_workers=%zu\n", delivered, n, g.concurrent_workers());
       return delivered == n ? 0 : 1;
     }
+    if (mode == "bench") return bench(argc, argv);
     if (argc < 8) throw std::runtime_error("missing arguments");
     GpuWorkerGroupConfig cfg;
     cfg.storage_dir = argv[2];
     cfg.key_dir = argv[3];
     const std::string session = argv[4];
     const int schema = std::atoi(argv[5]);
-    cfg.schemas.push_back(parse_params(schema, argv[6]));
+    cfg.schemas = {parse_params(schema, argv[6])};
     if (const char *d = std::getenv("WG_DEVICE")) cfg.devices = {std::atoi(d)};
     GpuWorkerGroup g(cfg);
     Status st;
@@ -114,14 +246,14 @@ int main(int argc, char **argv) {
       t.session_uuid = {session};
       t.input_data_frame_ptr.pointer = {{argv[7]}, (uint32_t)std::stoul(argv[8])};
       t.output_data_frame_ptr = {{argv[9]}, (uint32_t)std::stoul(argv[8])};
-      t.crypto_key_ptr.schema_type = schema;
+      t.crypto_key_ptr.schema_type = static_cast<herd::common::SchemaType>(schema);
       t.circuit = parse_program(argc, argv, 10);
       st = run(g, t);
     } else if (mode == "reduce") {
       herd::common::ReduceTask t;
       t.session_uuid = {session};
       t.output_data_frame_ptr = {{argv[7]}, (uint32_t)std::stoul(argv[8])};
-      t.crypto_key_ptr.schema_type = schema;
+      t.crypto_key_ptr.schema_type = static_cast<herd::common::SchemaType>(schema);
       for (int i = 9; i < argc; ++i) {
         const std::string a = argv[i];
         if (a == "--") {

@@ -86,6 +86,18 @@ int fhe_dev_free(fhe_ctx *ctx, void *ptr);
 /* h2d returns once the host buffer may be reused; d2h returns once the data has arrived */
 int fhe_memcpy_h2d(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
 int fhe_memcpy_d2h(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* pinned (page-locked) HOST staging memory, and copies that only enqueue on the
+ * context's stream: the host buffer must come from fhe_host_alloc and stay
+ * untouched until the next fhe_synchronize (a worker stages the inputs of a
+ * batch while earlier copies and kernels run) */
+int fhe_host_alloc(fhe_ctx *ctx, size_t bytes, void **out);
+int fhe_host_free(fhe_ctx *ctx, void *ptr);
+int fhe_memcpy_h2d_async(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
+int fhe_memcpy_d2h_async(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* give the context a HIP stream of its own (non-blocking, destroyed with the
+ * context) for callers without a stream of their own: several contexts on one
+ * device then run concurrently, e.g. the worker group's lanes */
+int fhe_use_own_stream(fhe_ctx *ctx);
 
 /* ---- RNS primitives: data [n_polys][n_limbs][N]; limb l uses modulus mod_begin+l */
 int fhe_ntt_fwd(fhe_ctx *ctx, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs);
