@@ -1,31 +1,51 @@
 #!/usr/bin/env python3
 """Headline benchmark: CKKS ct-mult+relin/s at N=2^16, L=12 (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch G] [--batch B]
 
-One step = one fhe_mul_relin call over B independent ciphertext pairs per GPU
-(N=2^16, L=12 primes of 60 bits, K=4 special primes of 61 bits, dnum=3 hybrid
-key switching), inputs already resident in HBM (generated on device with the
-backend's SplitMix64 fill).  Multi-GPU: one process per GPU (torchrun), the
-relinearisation key is generated on rank 0 and broadcast once over RCCL
-(the only collective), then every rank works on its own shard with no
-communication ("scaling": "weak").  value = ct-mults of all ranks / max-rank time.
+Workload (BASELINE.json configs[4], "C5"): a batch of G = 8192 independent
+ct-mult+relin at N=2^16, L=12 primes of 60 bits, K=4 special primes of 61 bits,
+dnum=3 hybrid key switching.  The batch is sharded over the ranks with
+herdsman's partition rule (dist.shard_range: floor(G/N) each, +1 for the first
+G mod N ranks; /root/reference/src/service/storage_service.cpp:121-129), one
+process per GPU; every rank processes its shard in waves of B ct-mults, each
+wave split over S concurrent contexts (one HIP stream each).  One step = the
+whole G-ct batch; "scaling" is "strong" (total work fixed as N grows).
+
+Memory: 8192 ciphertext pairs plus outputs are 288 GiB, more than one GPU's
+HBM, so each rank keeps a resident pool of up to --pool distinct input pairs
+and output slots (36 GiB at 1024) generated ON THE DEVICE, and its waves walk
+through the pool (at N=8 a rank's 1024 ct-mults all have distinct inputs).
+Inputs are resident in HBM before the timed region; nothing is skipped inside it.
+
+Multi-GPU: `--gpus N` without a torchrun environment spawns N fresh worker
+processes (one per GPU, MASTER_ADDR 127.0.0.1) before anything touches the GPU;
+under torchrun (RANK/WORLD_SIZE set) the process is one rank.  Rank 0 generates
+the relinearisation key and broadcasts it once with fhe_bcast_key on PyTorch's
+RCCL communicator (the same librccl instance the backend binds to) -- the only
+collective; afterwards each rank works alone.  value = G * steps / max-rank time.
 
 Extra fields:
   roofline     -- the dominant kernel group, the forward NTT (column + row pass
-                  kernels, one fhe_ntt_fwd launch over the batch's limbs),
-                  timed with HIP events on the backend's stream; algorithmic
-                  bytes = 2 * N * 8 per limb-NTT (read + write the residue once).
-  cpu_baseline -- the CPU oracle (oracle/fhe_oracle.c, OpenMP over ciphertexts)
-                  on a bounded sample of the same workload, rank 0 at N=1 only.
-  secondary    -- per-GPU throughput of the other BASELINE configs: C4 rotate,
-                  C3 BFV mul+relin, C2 NTT (not part of `value`).
+                  kernels, one fhe_ntt_fwd launch over B*3*L limbs), timed with
+                  HIP events on the stream the kernels run on; algorithmic bytes
+                  = 2 * N * 8 per limb-NTT.  frac_rocprof recomputes the same
+                  fraction from the committed rocprofv3 kernel averages, and
+                  traffic is the PMC-counted HBM bytes (profiles/, see "profile").
+  cpu_baseline -- the CPU oracle (oracle/fhe_oracle.c, OpenMP, threads pinned) on
+                  a bounded sample of the same workload, in a child process on
+                  the host's cores (rank 0, N=1 only); also C2/C3/C4 samples.
+  secondary    -- per-GPU throughput of the other BASELINE configs (C4 rotate,
+                  C3 BFV mul+relin, C2 NTT) and the metric config on
+                  OpenFHE-style primes (generic Montgomery path).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
@@ -37,30 +57,85 @@ LOG_N, L, K, DNUM = 16, 12, 4, 3
 HBM_PEAK_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="ct-mults per GPU per step")
-    ap.add_argument("--ntt-reps", type=int, default=20)
-    ap.add_argument("--cpu-sample", type=int, default=4096, help="max ct-mults in the CPU baseline sample")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline duration")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--graph", type=int, default=0, help="1: replay the step from a captured HIP graph")
+    ap.add_argument("--global-batch", type=int, default=8192, help="ct-mults per step over all ranks (C5)")
+    ap.add_argument("--batch", type=int, default=128, help="ct-mults per wave per GPU")
+    ap.add_argument("--pool", type=int, default=1024, help="distinct resident input pairs per GPU")
     ap.add_argument("--streams", type=int, default=4,
-                    help="contexts (one HIP stream each) that share a step's batch and run concurrently")
+                    help="contexts (one HIP stream each) that share a wave and run concurrently")
+    ap.add_argument("--ntt-reps", type=int, default=20)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline duration (metric)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may use")
+    ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the secondary measurements (C4 rotate, C3 BFV mul+relin, C2 NTT)")
+                    help="skip the secondary measurements (C4 rotate, C3 BFV, C2 NTT, generic moduli)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the timed NTT loop (for rocprofv3 runs of the dominant kernel)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "ntt_traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / sharding / timing control flow only, on CPU (gloo), no GPU work")
+    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "ntt_traffic.json"))
+    return ap.parse_args(argv)
 
 
+# ------------------------------------------------------------------ launcher
+def launch(args) -> int:
+    """Parent of an N-GPU run started without torchrun: spawn one fresh process
+    per GPU (this process never initialises the GPU), wait, relay the exit code.
+    If a rank fails, the others are stopped (they would wait in a collective)."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def _rccl_comm(dev):
+    """ncclComm_t of PyTorch's RCCL process group on `dev` (0 if unavailable): the
+    backend's fhe_bcast_key must use a communicator of the librccl instance it
+    is bound to, which in a torch process is torch's own."""
+    import torch.distributed as dist
+    try:
+        be = dist.group.WORLD._get_backend(dev)
+        return int(be._comm_ptr()) if hasattr(be, "_comm_ptr") else 0
+    except Exception:
+        return 0
+
+
+# -------------------------------------------------------------------- ranks
 def main():
     args = parse()
+    if args.cpu_baseline_child:
+        print(json.dumps(cpu_baseline_child(args)), flush=True)
+        return 0
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args)
+    if args.dry_run:
+        return dry_run(args)
+
     import torch
     import torch.distributed as dist
 
@@ -80,20 +155,22 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    devices = [gpu]
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, gpu)
+    n_gpus = len(set(devices))
 
+    # ---- shard of the C5 batch and its wave / pool geometry
+    G = args.global_batch
+    my, B, S, waves, P, Bs, plan = wave_plan(G, args.batch, args.streams, args.pool, world, rank)
+    full_secondary = world == 1 and not (args.roofline_only or args.no_secondary)
+
+    n = 1 << LOG_N
     ctx = hb.Context(hb.SCHEME_CKKS, LOG_N, L, K, DNUM, device=gpu)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream)
-    n = 1 << LOG_N
-    B = args.batch
-    # S concurrent contexts, one HIP stream each, split the step's batch: kernels of
-    # different stages (VALU-bound NTT passes, HBM-bound conversions) overlap across
-    # the GPU's hardware queues (4 x 32 vs 1 x 128: +5%)
-    S = 1 if args.graph else max(1, min(args.streams, B))
-    if B % S:
-        raise SystemExit(f"--batch {B} is not a multiple of --streams {S}")
-    Bs = B // S
-    ctx.reserve(B)
+    ctx.reserve(B if full_secondary else Bs)  # the secondary calls run whole waves on lane 0
     lanes = [(ctx, stream)]
     for _ in range(S - 1):
         c_i = hb.Context(hb.SCHEME_CKKS, LOG_N, L, K, DNUM, device=gpu)
@@ -102,39 +179,36 @@ def main():
         c_i.reserve(Bs)
         lanes.append((c_i, s_i))
 
-    # relinearisation key: rank 0 makes it, RCCL broadcast to everyone else
+    # ---- relinearisation key: rank 0 makes it, one RCCL broadcast to the others
     rlk = hb.empty(ctx.key_shape(), device=dev)
     if rank == 0:
         ctx.fill_uniform(rlk, seed=0x524C4B)
     torch.cuda.synchronize(dev)
+    bcast = "none (1 rank)"
+    if world > 1:
+        dist.barrier()
     t_b = time.perf_counter()
-    broadcast_key(rlk, src=0)  # the only collective: RCCL over xGMI
+    if world > 1:
+        comm = _rccl_comm(dev) if backend == "nccl" else 0
+        if comm:
+            ctx.bcast_key(rlk, comm, root=0)  # fhe_bcast_key: ncclBroadcast over xGMI
+            bcast = "fhe_bcast_key (RCCL)"
+        else:
+            broadcast_key(rlk, src=0)
+            bcast = f"torch.distributed.broadcast ({backend})"
     torch.cuda.synchronize(dev)
     key_bcast_ms = (time.perf_counter() - t_b) * 1e3
 
-    a = hb.empty((B, 2, L, n), device=dev)
-    b = hb.empty((B, 2, L, n), device=dev)
-    out = hb.empty((B, 2, L, n), device=dev)
+    a = hb.empty((P, 2, L, n), device=dev)
+    b = hb.empty((P, 2, L, n), device=dev)
+    out = hb.empty((P, 2, L, n), device=dev)
     ctx.fill_uniform(a, seed=0x48455244 ^ (rank << 32) ^ 1)
     ctx.fill_uniform(b, seed=0x48455244 ^ (rank << 32) ^ 2)
-
     torch.cuda.synchronize(dev)  # inputs were filled on the first context's stream
 
     def step():
-        for i, (c_i, _) in enumerate(lanes):
-            c_i.mul_relin(a[i * Bs:(i + 1) * Bs], b[i * Bs:(i + 1) * Bs], rlk, out[i * Bs:(i + 1) * Bs])
-
-    if args.graph and not args.roofline_only:
-        # capture one step (~25 kernel launches) into a HIP graph and replay it:
-        # the workspace was pre-sized by ctx.reserve, so nothing allocates
-        ctx.mul_relin(a, b, rlk, out)  # warm
-        torch.cuda.synchronize(dev)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            ctx.set_stream(torch.cuda.current_stream(dev))
-            ctx.mul_relin(a, b, rlk, out)
-        ctx.set_stream(stream)
-        step = graph.replay
+        for i, lo, hi in plan:
+            lanes[i][0].mul_relin(a[lo:hi], b[lo:hi], rlk, out[lo:hi])
 
     steps = 0 if args.roofline_only else args.steps
     for _ in range(0 if args.roofline_only else args.warmup):
@@ -147,93 +221,169 @@ def main():
     for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
+    mine = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
-    total = world * B * steps
-    value = total / elapsed if steps else 0.0
+    elapsed = max_over_ranks(mine, device=dev)
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, (my * steps / mine) if mine > 0 else 0.0)
+    else:
+        per_rank = [(my * steps / mine) if mine > 0 else 0.0]
+    value = G * steps / elapsed if steps else 0.0
 
-    # ---- dominant kernel group: forward NTT over the ModUp-sized batch (36 limbs per ct)
-    limbs = B * 3 * L  # the converted limbs of one batch's ModUp
-    x = hb.empty((limbs, 1, n), device=dev)
-    ctx.fill_uniform(x.view(B * 3, L, n), seed=99)
+    # ---- dominant kernel group: forward NTT over the ModUp-sized wave (36 limbs per ct)
+    limbs = B * 3 * L
+    x = hb.empty((B * 3, L, n), device=dev)
+    ctx.fill_uniform(x, seed=99)
     for _ in range(3):
-        ctx.ntt_fwd(x.view(B * 3, L, n))
+        ctx.ntt_fwd(x)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
+    e0.record(stream)  # the stream the NTT kernels are launched on (ctx.set_stream above)
     reps = max(1, args.ntt_reps)
     for _ in range(reps):
-        ctx.ntt_fwd(x.view(B * 3, L, n))
+        ctx.ntt_fwd(x)
     e1.record(stream)
     e1.synchronize()
     ntt_ms = e0.elapsed_time(e1) / reps
-    algo_bytes = limbs * 2 * n * 8
+    del x
+    algo_per_limb = 2 * n * 8
+    algo_bytes = limbs * algo_per_limb
     achieved = algo_bytes / (ntt_ms * 1e-3) / 1e9
-    traffic = valu_busy = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            traffic = tj.get("hbm_bytes_per_limb_ntt")
-            valu_busy = tj.get("valu_busy")
-            if traffic is not None:
-                traffic = traffic * limbs
-        except Exception:
-            traffic = None
-    ntt_limb_per_s = limbs / (ntt_ms * 1e-3)
+    roof = {
+        "kernel": "ntt_fwd (ntt_pass col + row), N=2^16",
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "algorithmic_bytes": algo_bytes,
+        "launch_ms": round(ntt_ms, 4),
+    }
+    roof.update(profile_fields(args.profile_json, limbs, algo_per_limb))
 
     secondary = None
-    if not (args.roofline_only or args.no_secondary):
-        secondary = secondary_configs(hb, ctx, rlk, a, out, dev, stream, B, max(2, args.steps // 2))
+    if full_secondary:
+        secondary = secondary_configs(hb, ctx, rlk, a, b, out, dev, stream, B, max(2, args.steps // 2))
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, ctx)
+    if rank == 0 and world == 1 and not (args.no_cpu or args.roofline_only):
+        cpu = run_cpu_baseline(args)
 
     if rank == 0:
         line = {
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "ct-mult/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / max(steps, 1) * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic: uniform residues mod q (on-device SplitMix64), uniform relin key",
             "config": {
-                "workload": "ckks_mul_relin",
+                "workload": f"C5: {G} independent CKKS ct-mult+relin per step, sharded over {world} rank(s)",
                 "log_n": LOG_N, "L": L, "K": K, "dnum": DNUM,
                 "q_bits": 60, "p_bits": 61,
-                "batch_per_gpu": B, "global_batch": B * world,
-                "parallelism": f"shard{world}", "streams_per_gpu": S,
+                "global_batch": G, "batch_per_gpu": my, "wave": B, "waves_per_step": waves,
+                "resident_pool": P, "streams_per_gpu": S,
+                "parallelism": f"shard{world}", "ranks": world,
             },
-            "roofline": {
-                "kernel": "ntt_fwd (ntt_pass col + row), N=2^16",
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes": algo_bytes,
-                "launch_ms": round(ntt_ms, 4),
-                # the NTT is integer-VALU bound, not HBM bound: share of the
-                # SIMDs' issue slots running VALU work (PMC, profiles/)
-                "valu_busy": valu_busy,
-            },
-            "ntt_fwd_limb_per_s": round(ntt_limb_per_s, 1),
+            "roofline": roof,
+            "ntt_fwd_limb_per_s": round(limbs / (ntt_ms * 1e-3), 1),
+            "per_rank_ct_mult_per_s": [round(v, 1) for v in per_rank],
             "key_bcast_ms": round(key_bcast_ms, 3),
-            "algorithmic_GBps_ct_mult": round(value / world * 6 * L * n * 8 / 1e9, 1),
+            "key_bcast_via": bcast,
+            "algorithmic_GBps_ct_mult": round(value / n_gpus * 6 * L * n * 8 / 1e9, 1),
             "cpu_baseline": cpu,
             "secondary": secondary,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def wave_plan(G, batch, streams, pool, world, rank):
+    """This rank's shard of a G-ct batch (herdsman's partition rule) as waves of
+    `batch` ct-mults over `streams` lanes, on a resident pool of P slots (a
+    multiple of the wave).  Returns (my, B, S, waves, P, Bs, plan) with plan =
+    [(lane, lo, hi)] pool slices in issue order."""
+    from herdsman_amd.dist import shard_range
+
+    b0, b1 = shard_range(G, world, rank)
+    my = b1 - b0
+    B = max(1, min(batch, my)) if my else 1
+    S = max(1, min(streams, B))
+    waves = math.ceil(my / B) if my else 0
+    P = min(max(pool // B, 1), max(waves, 1)) * B
+    Bs = math.ceil(B / S)
+    plan = []
+    for w in range(waves):
+        cnt = min(B, my - w * B)
+        o = (w * B) % P
+        for i in range(S):
+            lo, hi = o + i * Bs, min(o + (i + 1) * Bs, o + cnt)
+            if lo < hi:
+                plan.append((i, lo, hi))
+    return my, B, S, waves, P, Bs, plan
+
+
+def dry_run(args):
+    """The multi-rank control flow without a GPU (tests/test_multi_rank.py): process
+    group (gloo), shard / wave plan, barriers, max-over-ranks timing, rank-0 line."""
+    import torch.distributed as dist
+
+    from herdsman_amd.dist import max_over_ranks
+    from herdsman_amd.dist import world as dist_world
+
+    rank, local, world = dist_world()
+    if world > 1:
+        dist.init_process_group("gloo")
+    my, B, S, waves, P, Bs, plan = wave_plan(args.global_batch, args.batch, args.streams, args.pool, world, rank)
+    covered = sum(hi - lo for _, lo, hi in plan)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    shards = [(rank, my, covered, os.getpid())]
+    if world > 1:
+        shards = [None] * world
+        dist.all_gather_object(shards, (rank, my, covered, os.getpid()))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "ranks": world, "shards": shards, "wave": B, "waves": waves,
+                          "pool": P, "lanes": S, "elapsed": elapsed}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def profile_fields(path, limbs, algo_per_limb):
+    """The committed rocprofv3 evidence for the roofline kernels (tools/collect_profile.py):
+    the kernel-trace average launch time -> frac_rocprof, the PMC bytes -> traffic."""
+    try:
+        pj = json.load(open(path))
+    except (OSError, ValueError):
+        return {"profile": None}
+    res = {"profile": pj.get("source")}
+    per_limb = pj.get("hbm_bytes_per_limb_ntt")
+    if per_limb:
+        res["traffic"] = round(per_limb * limbs)
+        res["traffic_per_limb_ntt"] = round(per_limb)
+    launch_ns, plimbs = pj.get("ntt_fwd_launch_ns"), pj.get("limbs_per_launch")
+    if launch_ns and plimbs:
+        res["rocprof_launch_ms"] = round(launch_ns / 1e6, 4)
+        res["frac_rocprof"] = round(plimbs * algo_per_limb / (launch_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+    if pj.get("valu_busy") is not None:
+        res["valu_busy"] = pj["valu_busy"]
+    return res
 
 
 def _timed(fn, reps, stream):
@@ -248,14 +398,32 @@ def _timed(fn, reps, stream):
     return e0.elapsed_time(e1) / reps * 1e-3
 
 
-def secondary_configs(hb, ctx, gk, ct, out, dev, stream, B, reps):
+def secondary_configs(hb, ctx, gk, a, b, out, dev, stream, B, reps):
     """Per-GPU throughput of the other BASELINE.json configs (same synthetic-data rules):
     C4 CKKS rotate + hybrid KS at the metric parameters (B ciphertexts per call),
-    C3 BFV mul+relin at N=2^15 L=8 (BEHZ), C2 forward+inverse NTT at N=2^14 L=4."""
+    C3 BFV mul+relin at N=2^15 L=8 (BEHZ), C2 forward+inverse NTT at N=2^14 L=4, and
+    the metric op on OpenFHE-style primes (q = 1 mod 2N, generic Montgomery path)
+    next to the same single-context call on the default primes."""
+    from herdsman_amd.params import openfhe_style_primes
+
     res = {}
     g = ctx.galois_elt(1)
-    t = _timed(lambda: ctx.rotate(ct, g, gk, out), reps, stream)
+    ct, o = a[:B], out[:B]
+    t = _timed(lambda: ctx.rotate(ct, g, gk, o), reps, stream)
     res["C4_ckks_rotate_per_s"] = round(B / t, 1)
+    t = _timed(lambda: ctx.mul_relin(ct, b[:B], gk, o), reps, stream)
+    res["C5_mul_relin_1ctx_per_s"] = round(B / t, 1)
+    mods = openfhe_style_primes([(60, L), (61, K)], LOG_N)
+    gen = hb.Context(hb.SCHEME_CKKS, LOG_N, L, K, DNUM, moduli=mods, device=dev.index)
+    gen.set_stream(stream)
+    gen.reserve(B)
+    ga = gen.fill_uniform(hb.empty((B, 2, L, 1 << LOG_N), device=dev), seed=41)
+    gb = gen.fill_uniform(hb.empty((B, 2, L, 1 << LOG_N), device=dev), seed=42)
+    gkey = gen.fill_uniform(hb.empty(gen.key_shape(), device=dev), seed=43)
+    t = _timed(lambda: gen.mul_relin(ga, gb, gkey, o), reps, stream)
+    res["C5_mul_relin_openfhe_primes_1ctx_per_s"] = round(B / t, 1)
+    del ga, gb, gkey
+    gen.close()
     bfv = hb.Context(hb.SCHEME_BFV, 15, 8, 4, 2, t=65537, device=dev.index)
     bfv.set_stream(stream)
     n3 = 1 << 15
@@ -278,34 +446,95 @@ def secondary_configs(hb, ctx, gk, ct, out, dev, stream, B, reps):
     return res
 
 
-def cpu_baseline(args, ctx):
-    """CPU oracle (test infrastructure) on a bounded sample of the same workload."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle_ffi import Oracle, SCHEME_CKKS
+# --------------------------------------------------------------- CPU baseline
+def _host_cores():
+    """(cores this process may use, nproc, cgroup CPU quota or None, CPU model)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    return cores, aff, quota, model
 
-    o = Oracle(SCHEME_CKKS, LOG_N, L, K, DNUM, moduli=ctx.moduli)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+
+def run_cpu_baseline(args):
+    """The oracle in a child process (no GPU, no torch) so that its OpenMP threads
+    can be pinned (OMP_PROC_BIND / OMP_PLACES are read when libgomp starts)."""
+    cores, aff, quota, model = _host_cores()
+    threads = args.cpu_threads or cores
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--cpu-threads", str(threads),
+           "--cpu-seconds", str(args.cpu_seconds)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res.update({"cores": threads, "nproc": aff, "cgroup_cpu_quota": quota, "cpu_model": model,
+                "pinning": "OMP_PROC_BIND=close OMP_PLACES=cores"})
+    return res
+
+
+def cpu_baseline_child(args):
+    """CPU oracle (test infrastructure) on bounded samples of the bench workloads."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_ffi import Oracle, SCHEME_BFV, SCHEME_CKKS
+
+    threads = max(1, args.cpu_threads)
+
+    def timed(fn, per_call, seconds):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            done += per_call
+            dt = time.perf_counter() - t0
+            if dt >= seconds and done >= 2 * per_call:
+                return done, dt
+
+    o = Oracle(SCHEME_CKKS, LOG_N, L, K, DNUM)
     o.lib.orc_set_threads(threads)
-    s = max(threads, 1)
-    a = o.uniform((s, 2, L, 1 << LOG_N), seed=1)
-    b = o.uniform((s, 2, L, 1 << LOG_N), seed=2)
+    a = o.uniform((threads, 2, L, 1 << LOG_N), seed=1)
+    b = o.uniform((threads, 2, L, 1 << LOG_N), seed=2)
     k = o.uniform(o.key_shape(), seed=3)
-    done, t0 = 0, time.perf_counter()
-    while True:  # ~args.cpu_seconds of CPU work, at least two rounds
-        o.mul_relin(a, b, k)
-        done += s
-        dt = time.perf_counter() - t0
-        if (dt >= args.cpu_seconds and done >= 2 * s) or done >= args.cpu_sample:
-            break
-    return {
+    done, dt = timed(lambda: o.mul_relin(a, b, k), threads, args.cpu_seconds)
+    res = {
         "value": round(done / dt, 3),
         "unit": "ct-mult/s",
-        "cores": threads,
         "kind": "port",
         "sample": f"{done} CKKS ct-mult+relin at N=2^16 L=12 K=4 dnum=3 in {dt:.1f} s "
-                  f"(batches of {s}, OpenMP one ciphertext per thread)",
+                  f"(batches of {threads}, OpenMP one ciphertext per thread)",
     }
+    sec = {}
+    g = o.galois_elt(1)
+    done, dt = timed(lambda: o.rotate(a, g, k), threads, 3.0)
+    sec["C4_ckks_rotate_per_s"] = round(done / dt, 3)
+    del a, b, k
+    o3 = Oracle(SCHEME_BFV, 15, 8, 4, 2, t=65537)
+    a3 = o3.uniform((threads, 2, 8, 1 << 15), seed=31)
+    b3 = o3.uniform((threads, 2, 8, 1 << 15), seed=32)
+    k3 = o3.uniform(o3.key_shape(), seed=33)
+    done, dt = timed(lambda: o3.mul_relin(a3, b3, k3), threads, 3.0)
+    sec["C3_bfv_mul_relin_per_s"] = round(done / dt, 3)
+    del a3, b3, k3
+    o2 = Oracle(SCHEME_CKKS, 14, 4)
+    polys = 4 * threads
+    x2 = o2.uniform((polys, 4, 1 << 14), seed=21)
+    done, dt = timed(lambda: o2.ntt_inv(o2.ntt_fwd(x2)), polys, 3.0)
+    sec["C2_ntt_fwd_inv_poly_per_s"] = round(done / dt, 3)
+    res["secondary"] = sec
+    return res
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

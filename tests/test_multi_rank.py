@@ -142,3 +142,45 @@ def test_reduce_schedule_is_a_tree():
                 assert len(sends[r]) == 1 and sched[r][-1][0] == "send"
                 assert ("recv", r) in sched[sends[r][0]]
             assert sum(len(s) for s in sched.values()) == 2 * (world - 1)
+
+
+# ------------------------------------------------------- bench.py multi-rank launcher
+def test_bench_launcher_spawns_ranks_dry_run():
+    """`bench.py --gpus 2` outside torchrun spawns 2 fresh rank processes (the
+    parent never touches a GPU); the ranks form a gloo group, split the C5 batch
+    of 8192 with herdsman's rule and time with max-over-ranks (--dry-run: the
+    control flow without GPU work)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["ranks"] == 2
+    shards = sorted(line["shards"])
+    assert [s[1] for s in shards] == [4096, 4096] and all(s[1] == s[2] for s in shards)
+    assert len({s[3] for s in shards}) == 2  # two processes
+    assert line["elapsed"] >= 0.02  # the slower rank's time
+
+
+def test_wave_plan_covers_each_shard_once():
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for G, world, batch, streams, pool in [(8192, 1, 128, 4, 1024), (8192, 8, 128, 4, 1024), (8192, 3, 128, 4, 1024),
+                                           (1000, 7, 64, 3, 100), (5, 8, 128, 4, 1024)]:
+        total = 0
+        for rank in range(world):
+            my, B, S, waves, P, Bs, plan = bench.wave_plan(G, batch, streams, pool, world, rank)
+            assert sum(hi - lo for _, lo, hi in plan) == my
+            assert all(0 <= lo < hi <= P and 0 <= i < S and hi - lo <= Bs for i, lo, hi in plan)
+            assert P % B == 0 and P <= max(pool, B) * 1 + B
+            total += my
+        assert total == G
