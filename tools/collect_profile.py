@@ -25,7 +25,7 @@ def short(name):
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
-    for tag in ("roofline", "bench"):
+    for tag in ("roofline", "bench", "bench4"):
         f = glob.glob(f"{src}/{tag}/*kernel_stats.csv")
         if f:
             shutil.copy(f[0], f"{dst}/{tag}_kernel_stats.csv")
@@ -54,6 +54,15 @@ def main(src, dst):
             valu.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
             rows.append({"kernel": k, "counter": r["Counter_Name"], "value": r["Counter_Value"],
                          "grid": r["Grid_Size"]})
+    # instruction mix per limb-NTT (the PMC table VERDICT r1 asked for)
+    mix = {}
+    for tag in ("pmc_valu", "pmc_mix"):
+        for f in glob.glob(f"{src}/{tag}/*counter_collection.csv"):
+            for r in csv.DictReader(open(f)):
+                if "ntt_pass" not in r["Kernel_Name"]:
+                    continue
+                mix.setdefault(short(r["Kernel_Name"]), {}).setdefault(r["Counter_Name"], []).append(
+                    float(r["Counter_Value"]))
     valu_busy = {}
     for k, cs in valu.items():
         mean = {n: sum(v) / len(v) for n, v in cs.items()}
@@ -78,7 +87,9 @@ def main(src, dst):
         w.writerows(rows)
     vb = (sum(valu_busy[k] * ntt.get(k, 0) for k in valu_busy) / sum(ntt.get(k, 0) for k in valu_busy)
           if valu_busy else None)
-    summary = {"ntt_pass_avg_ns": ntt, "valu_busy": valu_busy, "valu_busy_launch": vb, "ntt_fwd_launch_ns": launch_ns, "limbs_per_launch": limbs,
+    per_limb_mix = {k: {n: sum(v) / len(v) / limbs for n, v in cs.items() if n.startswith("SQ_INSTS")}
+                    for k, cs in mix.items()}
+    summary = {"ntt_pass_avg_ns": ntt, "instructions_per_limb_ntt": per_limb_mix, "valu_busy": valu_busy, "valu_busy_launch": vb, "ntt_fwd_launch_ns": launch_ns, "limbs_per_launch": limbs,
                "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
                "hbm_bytes_per_limb_ntt": per_limb,
                "algorithmic_bytes_per_limb_ntt": 2 * (1 << LOG_N) * 8,

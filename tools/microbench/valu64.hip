@@ -35,6 +35,9 @@ typedef uint64_t u64;
 #define B_CMP64(x) asm volatile("v_cmp_le_u64 vcc, %0, %1" : : "v"(x), "v"(k) : "vcc"); x += 1;
 #define B_MULHI(x) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(x) : "v"(a));
 #define B_MULLO(x) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(a));
+#define B_NOT(x) asm volatile("v_not_b32 %0, %0" : "+v"(x));
+#define B_BFI(x) asm volatile("v_bfi_b32 %0, %0, %1, %0" : "+v"(x) : "v"(a));
+#define B_MOV64(x) asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
 #define B_SUBCO(x) asm volatile("v_sub_co_u32 %0, s[40:41], %0, %1\n v_subb_co_u32 %0, s[40:41], %0, %1, s[40:41]" : "+v"(x) : "v"(a) : "s40", "s41");
 
 KERNEL(k_lshladd, B_LSHLADD)
@@ -45,6 +48,9 @@ KERNEL(k_cmp64, B_CMP64)
 KERNEL32(k_mulhi, B_MULHI)
 KERNEL32(k_mullo, B_MULLO)
 KERNEL32(k_subco, B_SUBCO)
+KERNEL32(k_not, B_NOT)
+KERNEL32(k_bfi, B_BFI)
+KERNEL32(k_mov, B_MOV64)
 
 int main() {
   const int threads = 256, blocks = 256 * 8;
@@ -68,5 +74,8 @@ int main() {
   run("v_mul_hi_u32", k_mulhi, 1);
   run("v_mul_lo_u32", k_mullo, 1);
   run("v_sub_co+v_subb sgpr (/instr)", k_subco, 2);
+  run("v_not_b32", k_not, 1);
+  run("v_bfi_b32", k_bfi, 1);
+  run("v_mov_b32", k_mov, 1);
   return 0;
 }
