@@ -307,24 +307,32 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
       }
     }
     run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
+    // negated reduction constants pinned in SGPRs, so each conditional
+    // subtraction is one v_lshl_add_u64 with a scalar operand (left to itself
+    // the compiler forms x - m as a v_subrev_co/v_subb_co borrow chain with
+    // s_nop hazard padding)
+    u64 nq1 = 0 - q, nq2 = 0 - q2, nq4 = 0 - 2 * q2;
+    asm("" : "+s"(nq1));
+    asm("" : "+s"(nq2));
+    asm("" : "+s"(nq4));
     if constexpr (PG::LAST) {
       if constexpr (!INV) {
         if (!a.lazy_out) {
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             u64 v = x[r];
-            if (WIDE) v = harvey_csub(v, 0 - 2 * q2);
-            x[r] = harvey_csub(harvey_csub(v, 0 - q2), 0 - q);
+            if (WIDE) v = harvey_csub(v, nq4);
+            x[r] = harvey_csub(harvey_csub(v, nq2), nq1);
           }
         }
       } else {
         if (a.noscale) {
 #pragma unroll
-          for (int r = 0; r < R; ++r) x[r] = harvey_csub(x[r], 0 - q);  // GS outputs are below 2q
+          for (int r = 0; r < R; ++r) x[r] = harvey_csub(x[r], nq1);  // GS outputs are below 2q
         } else {
           const u64 sc = a.ninv[mod];
 #pragma unroll
-          for (int r = 0; r < R; ++r) x[r] = harvey_csub(mont_mul<SP>(x[r], sc, mi), 0 - q);
+          for (int r = 0; r < R; ++r) x[r] = harvey_csub(mont_mul<SP>(x[r], sc, mi), nq1);
         }
       }
     }
@@ -343,7 +351,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
         const u64 v = lds[lr + kr + (kr >> 4)];
         if constexpr (EPI == EPI_COMBINE) {
           // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM
-          u64 ks = harvey_csub(mont_mul<SP>(sub_mod(pa[r], v, q), ep.pinv, mi), 0 - q);
+          u64 ks = harvey_csub(mont_mul<SP>(sub_mod(pa[r], v, q), ep.pinv, mi), nq1);
           if (ep.add) ks = add_mod(ks, pb[r], q);
           st_b(ep.out + kr, voff, ks);
         } else {

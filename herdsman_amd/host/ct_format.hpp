@@ -54,4 +54,42 @@ uint64_t moduli_digest(const uint64_t *moduli, uint32_t count);
 std::vector<std::vector<uint8_t>> read_partition(const std::filesystem::path &path);
 void write_partition(const std::filesystem::path &path, const std::vector<std::vector<uint8_t>> &rows);
 
+// A partition file mapped read-only: rows are views into the mapping (no
+// per-row allocation or copy; the worker stages them straight into pinned
+// memory).  Throws on a missing file or a truncated row.
+class PartitionView {
+ public:
+  explicit PartitionView(const std::filesystem::path &path);
+  ~PartitionView();
+  PartitionView(const PartitionView &) = delete;
+  PartitionView &operator=(const PartitionView &) = delete;
+  size_t size() const { return rows_.size(); }
+  const uint8_t *row(size_t i) const { return rows_[i].first; }
+  uint32_t row_len(size_t i) const { return rows_[i].second; }
+
+ private:
+  void *map_ = nullptr;
+  size_t bytes_ = 0;
+  std::vector<std::pair<const uint8_t *, uint32_t>> rows_;
+};
+
+// Output partition written through a temporary file renamed into place by
+// commit(): a task that fails half-way leaves no output behind.  Rows are
+// gathered with writev from caller memory (header + words), no staging copy.
+class PartitionWriter {
+ public:
+  explicit PartitionWriter(const std::filesystem::path &path);
+  ~PartitionWriter();
+  PartitionWriter(const PartitionWriter &) = delete;
+  PartitionWriter &operator=(const PartitionWriter &) = delete;
+  // one row = `parts` byte ranges, written as u32 length + the ranges
+  void append(const std::vector<std::pair<const void *, size_t>> &parts);
+  void commit();
+
+ private:
+  std::filesystem::path path_, tmp_;
+  int fd_ = -1;
+  bool done_ = false;
+};
+
 }  // namespace herdsman_gpu

@@ -1,7 +1,14 @@
 // gpu_worker_group.cpp -- see gpu_worker_group.hpp.
 #include "gpu_worker_group.hpp"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <cstring>
 #include <fstream>
@@ -52,6 +59,93 @@ void write_partition(const std::filesystem::path &path, const std::vector<std::v
     out.write(reinterpret_cast<const char *>(r.data()), len);
   }
   if (!out) throw std::runtime_error("write failed " + path.string());
+}
+
+PartitionView::PartitionView(const std::filesystem::path &path) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) throw std::runtime_error("cannot open partition " + path.string());
+  struct stat st {};
+  if (::fstat(fd, &st) != 0) {
+    ::close(fd);
+    throw std::runtime_error("cannot stat partition " + path.string());
+  }
+  bytes_ = (size_t)st.st_size;
+  if (bytes_) {
+    map_ = ::mmap(nullptr, bytes_, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    if (map_ == MAP_FAILED) {
+      map_ = nullptr;
+      ::close(fd);
+      throw std::runtime_error("cannot map partition " + path.string());
+    }
+    (void)::madvise(map_, bytes_, MADV_SEQUENTIAL);
+  }
+  ::close(fd);
+  const uint8_t *p = static_cast<const uint8_t *>(map_), *end = p + bytes_;
+  while (p < end) {
+    if (end - p < 4) throw std::runtime_error("truncated row header");
+    uint32_t len;
+    std::memcpy(&len, p, 4);
+    p += 4;
+    if ((size_t)(end - p) < len) throw std::runtime_error("truncated row");
+    rows_.emplace_back(p, len);
+    p += len;
+  }
+}
+
+PartitionView::~PartitionView() {
+  if (map_) ::munmap(map_, bytes_);
+}
+
+PartitionWriter::PartitionWriter(const std::filesystem::path &path) : path_(path) {
+  std::filesystem::create_directories(path.parent_path());
+  tmp_ = path;
+  tmp_ += ".tmp-" + std::to_string((unsigned long)::getpid()) + "-" +
+          std::to_string(std::hash<std::thread::id>{}(std::this_thread::get_id()));
+  fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd_ < 0) throw std::runtime_error("cannot create partition " + tmp_.string());
+}
+
+PartitionWriter::~PartitionWriter() {
+  if (fd_ >= 0) ::close(fd_);
+  if (!done_) ::unlink(tmp_.c_str());
+}
+
+void PartitionWriter::append(const std::vector<std::pair<const void *, size_t>> &parts) {
+  uint32_t len = 0;
+  for (const auto &pr : parts) len += (uint32_t)pr.second;
+  std::vector<iovec> iov;
+  iov.push_back(iovec{&len, 4});
+  for (const auto &pr : parts) iov.push_back(iovec{const_cast<void *>(pr.first), pr.second});
+  size_t todo = 4 + (size_t)len, first = 0;
+  while (todo) {
+    const ssize_t w = ::writev(fd_, iov.data() + first, (int)(iov.size() - first));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw std::runtime_error("write failed " + tmp_.string());
+    }
+    todo -= (size_t)w;
+    size_t adv = (size_t)w;
+    while (adv && first < iov.size()) {  // partial write: skip what went out
+      if (adv >= iov[first].iov_len) {
+        adv -= iov[first].iov_len;
+        ++first;
+      } else {
+        iov[first].iov_base = static_cast<char *>(iov[first].iov_base) + adv;
+        iov[first].iov_len -= adv;
+        adv = 0;
+      }
+    }
+  }
+}
+
+void PartitionWriter::commit() {
+  if (::close(fd_) != 0) {
+    fd_ = -1;
+    throw std::runtime_error("close failed " + tmp_.string());
+  }
+  fd_ = -1;
+  std::filesystem::rename(tmp_, path_);
+  done_ = true;
 }
 
 // ------------------------------------------------------------- device state
@@ -421,28 +515,26 @@ std::shared_ptr<KeySet> device_keys(std::mutex &m, std::map<std::pair<std::strin
 }
 
 // parse ciphertext k of a row
-const uint64_t *row_ct(const SchemaCtx &s, const std::vector<uint8_t> &row, uint32_t k) {
+// words of ciphertext k of a row (unaligned in the file: the caller memcpys them)
+const uint8_t *row_ct(const SchemaCtx &s, const uint8_t *row, uint32_t len, uint32_t k) {
   const size_t one = sizeof(CtHeader) + s.ct_words() * 8;
-  if (row.size() < (k + 1) * one) throw std::runtime_error("row holds fewer ciphertexts than the circuit reads");
+  if (len < (k + 1) * one) throw std::runtime_error("row holds fewer ciphertexts than the circuit reads");
   CtHeader h;
-  std::memcpy(&h, row.data() + k * one, sizeof(h));
+  std::memcpy(&h, row + k * one, sizeof(h));
   if (h.magic != kCtMagic || h.version != 1 || h.scheme != s.scheme || h.log_n != s.log_n || h.n_limbs != s.L ||
       h.moduli_digest != s.q_digest)
     throw std::runtime_error("ciphertext header does not match the schema context");
-  return reinterpret_cast<const uint64_t *>(row.data() + k * one + sizeof(CtHeader));
+  return row + k * one + sizeof(CtHeader);
 }
 
-std::vector<uint8_t> make_row(const SchemaCtx &s, const uint64_t *words) {
+CtHeader ct_header(const SchemaCtx &s) {
   CtHeader h;
   h.scheme = (uint8_t)s.scheme;
   h.domain = s.scheme == FHE_SCHEME_CKKS ? 1 : 0;
   h.log_n = s.log_n;
   h.n_limbs = s.L;
   h.moduli_digest = s.q_digest;
-  std::vector<uint8_t> row(sizeof(h) + s.ct_words() * 8);
-  std::memcpy(row.data(), &h, sizeof(h));
-  std::memcpy(row.data() + sizeof(h), words, s.ct_words() * 8);
-  return row;
+  return h;
 }
 
 const DevBuf &galois_key(const SchemaCtx &s, const KeySet &ks, int32_t steps, uint32_t *g) {
@@ -456,9 +548,8 @@ const DevBuf &galois_key(const SchemaCtx &s, const KeySet &ks, int32_t steps, ui
 // own pinned buffer and copied asynchronously, so the host gathers input k+1
 // while input k is on the wire and earlier kernels run; the batch ends with
 // one asynchronous copy back and one synchronisation.
-void eval_map_batch(LaneSchema &ls, const KeySet &ks, const std::vector<Instr> &prog,
-                    const std::vector<std::vector<uint8_t>> &rows, size_t r0, size_t n,
-                    std::vector<std::vector<uint8_t>> &out_rows) {
+void eval_map_batch(LaneSchema &ls, const KeySet &ks, const std::vector<Instr> &prog, const PartitionView &rows,
+                    size_t r0, size_t n, PartitionWriter &out) {
   const SchemaCtx &s = ls.s;
   const size_t cw = s.ct_words();
   std::vector<ArenaBuf> stack;
@@ -468,7 +559,8 @@ void eval_map_batch(LaneSchema &ls, const KeySet &ks, const std::vector<Instr> &
       case Op::PUSH_INPUT: {
         if (ls.in_stage.size() <= push) ls.in_stage.push_back(std::make_unique<Pinned>());
         uint64_t *host = reinterpret_cast<uint64_t *>(ls.in_stage[push++]->reserve(s.ctx, cw * n * 8));
-        for (size_t r = 0; r < n; ++r) std::memcpy(host + r * cw, row_ct(s, rows[r0 + r], ins.arg), cw * 8);
+        for (size_t r = 0; r < n; ++r)
+          std::memcpy(host + r * cw, row_ct(s, rows.row(r0 + r), rows.row_len(r0 + r), ins.arg), cw * 8);
         ArenaBuf d(*ls.arena, cw * n);
         ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, d.p, host, cw * n * 8), "h2d");
         stack.push_back(std::move(d));
@@ -509,7 +601,8 @@ void eval_map_batch(LaneSchema &ls, const KeySet &ks, const std::vector<Instr> &
   uint64_t *host = reinterpret_cast<uint64_t *>(ls.out_stage.reserve(s.ctx, cw * n * 8));
   ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, host, stack.back().p, cw * n * 8), "d2h");
   ck(s.ctx, fhe_synchronize(s.ctx), "batch sync");  // staging buffers are free again after this
-  for (size_t r = 0; r < n; ++r) out_rows.push_back(make_row(s, host + r * cw));
+  const CtHeader h = ct_header(s);
+  for (size_t r = 0; r < n; ++r) out.append({{&h, sizeof(h)}, {host + r * cw, cw * 8}});
 }
 
 std::filesystem::path frame_path(const std::filesystem::path &root, const herd::common::UUID &session,
@@ -537,14 +630,13 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         const std::vector<Instr> prog = lower_circuit(t.circuit);
         LaneSchema &ls = lane_schema(lane.schemas, config_, dev.id, schema);
         auto ks = device_keys(dev.keys_m, dev.keys, ls.s, config_.key_dir, t.session_uuid.as_string(), schema);
-        const auto rows = read_partition(frame_path(config_.storage_dir, t.session_uuid, t.input_data_frame_ptr.pointer));
-        std::vector<std::vector<uint8_t>> out;
-        out.reserve(rows.size());
+        const PartitionView rows(frame_path(config_.storage_dir, t.session_uuid, t.input_data_frame_ptr.pointer));
+        PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr));
         for (size_t r0 = 0; r0 < rows.size(); r0 += config_.max_batch) {
           const size_t n = std::min<size_t>(config_.max_batch, rows.size() - r0);
           eval_map_batch(ls, *ks, prog, rows, r0, n, out);
         }
-        write_partition(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr), out);
+        out.commit();
       } else {
         // ReduceTask: combine every row of every input partition into one
         // ciphertext with a balanced tree of batched ADDs (MUL_RELIN if the
@@ -557,15 +649,20 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         const bool mul = !prog.empty() && prog.front().op == Op::MUL_RELIN;
         std::shared_ptr<KeySet> ks;
         if (mul) ks = device_keys(dev.keys_m, dev.keys, s, config_.key_dir, t.session_uuid.as_string(), schema);
-        std::vector<std::vector<uint8_t>> all;
-        for (const auto &in : t.input_data_frame_ptrs)
-          for (auto &row : read_partition(frame_path(config_.storage_dir, t.session_uuid, in.pointer)))
-            all.push_back(std::move(row));
-        if (all.empty()) throw std::runtime_error("reduce over no rows");
-        const size_t cw = s.ct_words(), count = all.size();
+        std::vector<std::unique_ptr<PartitionView>> parts;
+        size_t count = 0;
+        for (const auto &in : t.input_data_frame_ptrs) {
+          parts.push_back(std::make_unique<PartitionView>(frame_path(config_.storage_dir, t.session_uuid, in.pointer)));
+          count += parts.back()->size();
+        }
+        if (count == 0) throw std::runtime_error("reduce over no rows");
+        const size_t cw = s.ct_words();
         if (ls.in_stage.empty()) ls.in_stage.push_back(std::make_unique<Pinned>());
         uint64_t *host = reinterpret_cast<uint64_t *>(ls.in_stage[0]->reserve(s.ctx, count * cw * 8));
-        for (size_t r = 0; r < count; ++r) std::memcpy(host + r * cw, row_ct(s, all[r], 0), cw * 8);
+        size_t r = 0;
+        for (const auto &pv : parts)
+          for (size_t i = 0; i < pv->size(); ++i, ++r)
+            std::memcpy(host + r * cw, row_ct(s, pv->row(i), pv->row_len(i), 0), cw * 8);
         ArenaBuf a(*ls.arena, count * cw);
         ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, a.p, host, count * cw * 8), "h2d");
         // balanced tree, one batched add / mul+relin per level (fhe_reduce)
@@ -574,7 +671,10 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         uint64_t *res = reinterpret_cast<uint64_t *>(ls.out_stage.reserve(s.ctx, cw * 8));
         ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, res, a.p, cw * 8), "d2h");
         ck(s.ctx, fhe_synchronize(s.ctx), "reduce sync");
-        write_partition(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr), {make_row(s, res)});
+        PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr));
+        const CtHeader h = ct_header(s);
+        out.append({{&h, sizeof(h)}, {res, cw * 8}});
+        out.commit();
       }
     } catch (const std::exception &) {
       st = Status::ERROR;  // no exception crosses the seam (executor.cpp:168-178 fails the job)

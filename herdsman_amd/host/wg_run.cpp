@@ -178,8 +178,8 @@ static int bench(int argc, char **argv) {
     return herd::common::task_t{t};
   };
   double best = 0;
-  for (int rep = 0; rep < 2; ++rep) {  // rep 0 warms contexts, keys and buffers
-    GpuWorkerGroup g(cfg);
+  GpuWorkerGroup g(cfg);  // one long-lived group, as in a server
+  for (int rep = 0; rep < 3; ++rep) {  // rep 0 warms contexts, keys, pinned and device buffers
     std::mutex m;
     std::condition_variable cv;
     int done = 0, errors = 0, next = 0, inflight = 0;
@@ -207,9 +207,9 @@ static int bench(int argc, char **argv) {
     const double rate = (double)parts * rows / dt;
     std::printf("bench rep %d: %d MapTasks x %d rows in %.3f s = %.1f ct-mult+relin/s (%zu workers)\n", rep, parts,
                 rows, dt, rate, g.concurrent_workers());
-    best = std::max(best, rate);
+    if (rep) best = std::max(best, rate);
   }
-  std::printf("bench: %.1f ct-mult+relin/s\n", best);
+  std::printf("bench: %.1f ct-mult+relin/s (warm group)\n", best);
   return 0;
 }
 
