@@ -73,6 +73,11 @@ struct fhe_ctx {
   u64 *d_r2 = nullptr;         // [nmod]     R^2 mod q (x -> x R)
   ConvTab *d_modup = nullptr;  // device array [ceil(L/alpha)], h scaled by R^2
   ConvTab moddown{};           // P -> Q, h scaled by R
+  // per-modulus INTT output constants for conversions fused into the next
+  // NTT (CKKS, 2^15 <= N, K <= 4): P limbs N^-1 (P/p_k)^-1 R, so INTT(acc_P)
+  // emits ModDown's canonical v_k directly (ntt_fwd_combine_launch PRO_CONV)
+  u64 *d_iscale = nullptr;     // [nmod]
+  bool fuse_moddown = false;
   std::vector<void *> blobs;   // device allocations owned by the context
   void *behz = nullptr;        // BEHZ device constants (BFV)
   // fhe_base_conv tables by (src ids, ~0, dst ids); their device arrays are
@@ -113,9 +118,13 @@ u64 host_to_mont(u64 x, u64 q);  // x * 2^64 mod q
 
 // NTT (ntt.hip)
 // noscale (inverse): no N^-1 multiply; lazy_out (forward): outputs below 8q, not canonical
-int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false, bool lazy_out = false);
+// scale (inverse): per-modulus output constants replacing N^-1 (d_iscale)
+int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false, bool lazy_out = false,
+               const u64 *scale = nullptr);
+// pro: the ModDown conversion of acc's P limbs (scaled by d_iscale) fused into
+// the column pass (PRO_CONV); null = conv already holds the converted limbs
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
-                           u64 *out, u32 add_mask);
+                           u64 *out, u32 add_mask, const ConvTab *pro = nullptr);
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *x, u64 *e, u32 nl, u32 mod_offset, u32 n);
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);

@@ -267,6 +267,21 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
     for (u32 i = 0; i < L; ++i) dst.push_back(i);
     c->moddown = make_conv_tab(c, src, dst, 1, c->fold_ninv);
     if (!c->d_pinv || !c->d_modup || !c->moddown.h) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
+    // ModDown fused into NTT(conv): INTT(acc_P)'s output constants carry the
+    // conversion's (P/p_k)^-1 and N^-1 (two-pass sizes, at most 4 sources)
+    c->fuse_moddown = c->fold_ninv && c->log_n >= 15 && c->K <= 4;
+    if (c->fuse_moddown) {
+      std::vector<u64> isc(c->nmod, 0);
+      for (u32 k = 0; k < c->K; ++k) {
+        const u64 pk = c->moduli[L + k];
+        u64 prod = 1;
+        for (u32 m = 0; m < c->K; ++m)
+          if (m != k) prod = hmul(prod, c->moduli[L + m] % pk, pk);
+        isc[L + k] = tomont(hmul(hinv(prod, pk), hinv((u64)c->n % pk, pk), pk), pk);
+      }
+      c->d_iscale = (u64 *)ctx_upload(c, isc.data(), sizeof(u64) * isc.size());
+      if (!c->d_iscale) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
+    }
   }
   if (p->scheme == FHE_SCHEME_BFV) {
     int rc = behz_setup(c);

@@ -40,6 +40,11 @@ struct NttArgs {
   // inverse only: leave out the N^-1 scaling (the consumer's conversion
   // constants carry it, fhe_ctx::fold_ninv); outputs stay canonical
   u32 noscale;
+  // inverse only: if set, the last pass multiplies by scale[mod] (Montgomery
+  // form) instead of N^-1: the per-source constant of a following base
+  // conversion rides on the transform (fhe_ctx::d_iscale), so its outputs are
+  // already the conversion's canonical v_i = [x (S/s_i)^-1]_{s_i}
+  const u64 *scale;
   // forward only: leave the outputs in the lazy range (below 8q < 2^63), for a
   // consumer whose Montgomery products accept any input below 2^63 (the KS
   // inner product on special moduli)
@@ -66,13 +71,22 @@ struct NttArgs {
   // permuted slots, writes the key-switch base t_out[ct][0] = sigma_g(c0) and
   // the own-digit ext slot sigma_g(c1) R, and transforms sigma_g(c1)
   u32 t_g;
+  // PRO_CONV (first (column) pass of a forward NTT): the pass's input limb is
+  // the fast base conversion y_m = sum_i v_i h[i][m] of c_ns canonical source
+  // limbs v_i at c_src[poly][c_src_first + i] (poly stride c_src_stride limbs),
+  // m = the active-limb index of the map; conv never makes an HBM round trip
+  const u64 *c_src;
+  const u64 *c_h;        // [ns][nd] ConvTab.h
+  u32 c_src_stride, c_src_first, c_ns, c_nd;
 };
 
 // EPI_COMBINE: epilogue of a forward last pass; PRO_TENSOR: prologue of an
 // inverse first (row) pass
 // PRO_BFVT: prologue of the inverse first (row) pass of the BFV tensor
 // product e = (a0 b0, a0 b1 + a1 b0, a1 b1) in one RNS base
-enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4 };
+// PRO_CONV: prologue of a forward first (column) pass, the base conversion
+// that produces its input
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, PRO_CONV = 5 };
 
 // per-workgroup epilogue / prologue operands (resolved once per limb)
 struct EpiRow {
@@ -85,6 +99,9 @@ struct EpiRow {
   u64 *o0, *o1, *ext;
   u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base; ext)
   u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is
+  const u64 *src;  // PRO_CONV: source limb 0 of this poly (limb i at src + i N)
+  u64 h[4];        // PRO_CONV: h[i][m] of this workgroup's target limb
+  u32 ns;
 };
 
 // LDS slot of element k of sub-transform w: one pad word per 16 words and per
@@ -326,11 +343,11 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
           }
         }
       } else {
-        if (a.noscale) {
+        if (a.noscale && !a.scale) {
 #pragma unroll
           for (int r = 0; r < R; ++r) x[r] = harvey_csub(x[r], nq1);  // GS outputs are below 2q
         } else {
-          const u64 sc = a.ninv[mod];
+          const u64 sc = a.scale ? a.scale[mod] : a.ninv[mod];
 #pragma unroll
           for (int r = 0; r < R; ++r) x[r] = harvey_csub(mont_mul<SP>(x[r], sc, mi), nq1);
         }
@@ -452,8 +469,25 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
   } else {
     using GF = Grp<S, LOGR, G0>;
     voff = (gb + (GF::k_thr(ts) << PG::LS)) << 3;
+    if constexpr (EPI == PRO_CONV) {
+      // the base conversion (conv_apply, oracle) of this element from the ns
+      // source limbs at the same position, 4 elements at a time
+      constexpr size_t NW = (size_t)1 << LOG_N;
 #pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = ld_d(data + ((size_t)GF::k_reg(r) << PG::LS), voff);
+      for (int c0 = 0; c0 < R; c0 += 4) {
+        u64 sv[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            sv[j][i] = i < (int)ep.ns ? ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff) : 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont<4, SP>(sv[j], ep.h, 1, ep.ns, mi);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[r] = ld_d(data + ((size_t)GF::k_reg(r) << PG::LS), voff);
+    }
   }
   // the final store uses the group-0 layout for row passes and the last
   // group's layout for column passes; recompute the offset for the latter
@@ -469,8 +503,9 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI>
 __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
-                    EPI == PRO_BFVT,
+                    EPI == PRO_BFVT || EPI == PRO_CONV,
                 "ntt_pass epilogues");
+  static_assert(EPI != PRO_CONV || (!INV && COLS), "the conversion prologue feeds a forward column pass");
   static_assert(EPI != EPI_COMBINE || (!INV && !COLS), "epilogues follow a forward row pass");
   static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT) || (INV && !COLS),
                 "prologues feed an inverse row pass");
@@ -484,7 +519,26 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   // quantity is scalar (SGPR) and element addresses are 32-bit offsets from a
   // scalar base (global_load ... saddr): no 64-bit VALU address arithmetic
   const u32 tid = threadIdx.x;
-  const u32 poly = blockIdx.y, act = blockIdx.z;
+  u32 bx = blockIdx.x, poly = blockIdx.y, act = blockIdx.z;
+  if constexpr (EPI == PRO_CONV) {
+    // the T target limbs of one source block (poly, column block) run on
+    // consecutive workgroup ids of ONE XCD (ids are dealt round-robin over the
+    // 8 XCDs), so the ns source limbs come from that XCD's L2 after the first
+    // read instead of being re-fetched from HBM once per target
+    const u32 cbs = gridDim.x, T = gridDim.z, nsb = gridDim.x * gridDim.y;
+    const u32 lin = blockIdx.x + cbs * (blockIdx.y + gridDim.y * blockIdx.z);
+    u32 sb;
+    if ((nsb & 7) == 0) {
+      const u32 rest = lin >> 3;
+      act = rest % T;
+      sb = (rest / T) * 8 + (lin & 7);
+    } else {
+      act = lin % T;
+      sb = lin / T;
+    }
+    bx = sb % cbs;
+    poly = sb / cbs;
+  }
   const u32 limb = limbmap_limb(a.map, act);
   const u32 mod = a.map.mod_offset + limb;
   u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
@@ -496,7 +550,7 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   // lanes: every wave access is four 128 B row segments
   u32 w, ts;
   if (COLS) { w = tid % W; ts = tid / W; } else { ts = tid % T; w = tid / T; }
-  const u32 u = blockIdx.x * W + w;
+  const u32 u = bx * W + w;
   const u32 hi = u >> PG::LS;
   const u32 gb = (hi << (S + PG::LS)) + (u & (stride - 1));
 
@@ -538,6 +592,12 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
     ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
     ep.g = a.t_g;
   }
+  if constexpr (EPI == PRO_CONV) {
+    ep.src = a.c_src + (((size_t)poly * a.c_src_stride + a.c_src_first) << LOG_N);
+    ep.ns = a.c_ns;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ep.h[i] = i < (int)a.c_ns ? a.c_h[(size_t)i * a.c_nd + act] : 0;
+  }
   if constexpr (SP && !INV) {
     // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)
     if (mi.q < (1ull << 60)) {
@@ -565,7 +625,7 @@ int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
 
 template <int LOG_N, int S, int W, bool COLS, int EPI = EPI_NONE>
 int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
-  if constexpr (EPI == EPI_COMBINE) {
+  if constexpr (EPI == EPI_COMBINE || EPI == PRO_CONV) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, false, true, EPI>(c, a, n_jobs)
                       : launch_one<LOG_N, S, W, COLS, false, false, EPI>(c, a, n_jobs);
@@ -596,11 +656,12 @@ int single_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
 }
 
 // column pass: stages [0, S1), stride N >> S1
+template <int EPI = EPI_NONE>
 int col_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
   switch (a.log_n) {
-    case 15: return launch_pass<15, 7, 32, true>(c, a, inv, n_jobs);
-    case 16: return launch_pass<16, 8, 16, true>(c, a, inv, n_jobs);
-    case 17: return launch_pass<17, 8, 16, true>(c, a, inv, n_jobs);
+    case 15: return launch_pass<15, 7, 32, true, EPI>(c, a, inv, n_jobs);
+    case 16: return launch_pass<16, 8, 16, true, EPI>(c, a, inv, n_jobs);
+    case 17: return launch_pass<17, 8, 16, true, EPI>(c, a, inv, n_jobs);
   }
   return fhe_fail(c, FHE_ERR_UNSUPPORTED, "col_pass: log_n");
 }
@@ -618,7 +679,7 @@ int row_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
 
 }  // namespace
 
-int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool lazy_out) {
+int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool lazy_out, const u64 *scale) {
   const u32 n_jobs = m.n_polys * m.cnt;
   if (n_jobs == 0) return FHE_OK;
   if (m.n_polys > 65535u) {
@@ -628,7 +689,7 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
       LimbMap sub = m;
       sub.base = m.base + (size_t)p0 * m.poly_stride * c->n;
       sub.n_polys = (m.n_polys - p0) < per ? (m.n_polys - p0) : per;
-      int rc = ntt_launch(c, sub, inverse, noscale, lazy_out);
+      int rc = ntt_launch(c, sub, inverse, noscale, lazy_out, scale);
       if (rc) return rc;
     }
     return FHE_OK;
@@ -640,6 +701,7 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
   a.ninv = c->d_ninv;
   a.log_n = c->log_n;
   a.noscale = inverse && noscale;
+  a.scale = inverse ? scale : nullptr;
   a.lazy_out = !inverse && lazy_out;
   if (c->log_n <= 14) return single_pass(c, a, inverse, n_jobs);
   int rc;
@@ -658,7 +720,7 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
 //   out[p][i] = (add_mask bit (p & 1) ? base[p][i] : 0) + (acc[p][i] - NTT(conv)[p][i]) P^-1  mod q_i
 // conv is transformed in place by the first pass only; acc rows have stride acc_stride limbs.
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
-                           u64 *out, u32 add_mask) {
+                           u64 *out, u32 add_mask, const ConvTab *pro) {
   const u32 L = c->L;
   const size_t N = c->n;
   const u32 per = 65535u;  // gridDim.y
@@ -681,7 +743,20 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
     if (c->log_n <= 14) {
       rc = single_pass<EPI_COMBINE>(c, a, false, n_jobs);
     } else {
-      if ((rc = col_pass(c, a, false, n_jobs))) return rc;
+      if (pro) {
+        // the ModDown conversion P -> Q as the column pass's prologue: the
+        // sources are acc's P limbs, already scaled by the INTT (d_iscale)
+        a.c_src = acc + (size_t)p0 * acc_stride * N;
+        a.c_src_stride = acc_stride;
+        a.c_src_first = L;
+        a.c_ns = pro->ns;
+        a.c_nd = pro->nd;
+        a.c_h = pro->h;
+        rc = col_pass<PRO_CONV>(c, a, false, n_jobs);
+      } else {
+        rc = col_pass(c, a, false, n_jobs);
+      }
+      if (rc) return rc;
       rc = row_pass<EPI_COMBINE>(c, a, false, n_jobs);
     }
     if (rc) return rc;

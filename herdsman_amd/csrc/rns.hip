@@ -614,6 +614,14 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   }
   // 4. inner product with the key
   if ((rc = SP_DISPATCH(c, inner_impl, c, ext, ksk, acc, n, ndig))) return rc;
+  // 5-6. ModDown for NTT-form results: INTT the P part with the conversion's
+  //      source constants as its output scale, then NTT(conv) with the P -> Q
+  //      conversion in its first pass and the combine in its last
+  //      (out = base + (acc_Q - conv) P^-1): conv never makes an HBM round trip
+  if (ntt_form && c->fuse_moddown) {
+    if ((rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale))) return rc;
+    return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, &c->moddown);
+  }
   // 5. ModDown: INTT the P part (all of Q u P for BFV), convert P -> Q
   if ((rc = ntt_launch(c, LimbMap{acc, QP, ntt_form ? K : QP, ntt_form ? L : 0, QP, 0, 0, 2 * n}, true,
                        ntt_form && c->fold_ninv)))
