@@ -203,6 +203,37 @@ HD u64 dot_mont(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModIn
   return res;
 }
 
+// The same sum, left in the lazy range [0, 4q) (special moduli) or [0, 2q)
+// (generic) -- the input range of the forward NTT (ntt.hip), so a conversion
+// whose outputs are transformed next skips the last two (one) conditional
+// subtractions; the residue is the same, the NTT's outputs are bit-identical.
+template <int NS, bool SP>
+HD u64 dot_mont_lazy(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
+  u64 res = 0;
+#pragma unroll
+  for (int c0 = 0; c0 < NS; c0 += 4) {
+    if (c0 < (int)ns) {
+      u64 part;
+      if (SP) {
+        u64 sum = 0;  // <= 4 products below 1.5q each
+#pragma unroll
+        for (int i = c0; i < c0 + 4 && i < NS; ++i)
+          if (i < (int)ns) sum += mont_mul<SP>(v[i], h[(size_t)i * hs], m);
+        part = csub(sum, 4 * m.q);  // < 4q
+        res = c0 == 0 ? part : csub(res + part, 4 * m.q);
+      } else {
+        U128 acc{0, 0};
+#pragma unroll
+        for (int i = c0; i < c0 + 4 && i < NS; ++i)
+          if (i < (int)ns) mac128(acc, v[i], h[(size_t)i * hs]);
+        part = mont_reduce<SP>(acc, m);  // < 2q
+        res = c0 == 0 ? part : csub(res + part, 2 * m.q);
+      }
+    }
+  }
+  return res;
+}
+
 // SplitMix64 stream shared with the oracle (orc_fill_uniform)
 HD u64 splitmix64(u64 z) {
   z ^= z >> 30;

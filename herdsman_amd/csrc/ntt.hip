@@ -482,7 +482,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
           for (int i = 0; i < 4; ++i)
             sv[j][i] = i < (int)ep.ns ? ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff) : 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont<4, SP>(sv[j], ep.h, 1, ep.ns, mi);
+        for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont_lazy<4, SP>(sv[j], ep.h, 1, ep.ns, mi);  // < 4q
       }
     } else {
 #pragma unroll

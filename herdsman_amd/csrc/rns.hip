@@ -80,7 +80,9 @@ __device__ __forceinline__ void conv_stage(ConvLds<NS> &sh, const ConvTab &t, co
 // y_m = sum_i v_i h[i][m] for every target m, streamed to out[slot(m) * N]
 // (slot = the target's modulus id when by_mod, else m), for the CPT
 // coefficients of this thread (at stride EW_BLOCK)
-template <int NS, bool SP, int CPT>
+// LAZY: outputs in the forward NTT's input range (dot_mont_lazy), for a
+// conversion transformed next (ModUp)
+template <int NS, bool SP, int CPT, bool LAZY = false>
 __device__ __forceinline__ void conv_store(const ConvLds<NS> &sh, const u64 (&v)[CPT][NS], u32 ns, u32 nd, u64 *out,
                                            size_t N, bool by_mod, u32 mod_base) {
 #pragma unroll 1
@@ -91,7 +93,9 @@ __device__ __forceinline__ void conv_store(const ConvLds<NS> &sh, const u64 (&v)
     mi.qinv_neg = sh.aux[m];
     u64 *o = out + (by_mod ? sh.dm[m] - mod_base : m) * N;
 #pragma unroll
-    for (int c = 0; c < CPT; ++c) st_nt(o + c * EW_BLOCK, dot_mont<NS, SP>(v[c], sh.h + m, nd, ns, mi));
+    for (int c = 0; c < CPT; ++c)
+      st_nt(o + c * EW_BLOCK, LAZY ? dot_mont_lazy<NS, SP>(v[c], sh.h + m, nd, ns, mi)
+                                   : dot_mont<NS, SP>(v[c], sh.h + m, nd, ns, mi));
   }
 }
 
@@ -166,7 +170,8 @@ __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__
   u64 v[CONV_CPT][NS];
   conv_scale<NS, SP>(v, x, t, mods, nullptr, lo);
   __syncthreads();
-  conv_store<NS, SP, CONV_CPT>(sh, v, t.ns, t.nd, ext + ((size_t)(ct * ndig + j) * QP) * N + k, N, true, 0);
+  // the converted limbs go straight into the forward NTT: lazy range suffices
+  conv_store<NS, SP, CONV_CPT, true>(sh, v, t.ns, t.nd, ext + ((size_t)(ct * ndig + j) * QP) * N + k, N, true, 0);
 }
 
 // KS preparation for an input d (fhe_keyswitch, BFV): dc = d and the own-digit
