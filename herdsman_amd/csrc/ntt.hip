@@ -184,8 +184,9 @@ __device__ __forceinline__ u64 harvey_csub(u64 x, u64 neg_m) {
 }
 
 // Forward lazy-range schedule.  NARROW (every modulus): values in [0,4q)
-// between stages, U = csub(X, 2q) at every stage (Harvey).  WIDE (special
-// moduli q < 2^60, i.e. 8q < 2^63, the Montgomery input bound): a stage with
+// between stages, U = csub(X, 2q) at every stage (Harvey).  WIDE (moduli
+// q < 2^60, i.e. 8q < 2^63, the Montgomery input bound; the special product
+// is below 1.5q, the generic one below 2q): a stage with
 // input bound B q gives outputs below (B+2) q without any reduction
 // (X' = X + V < (B+1.5) q, Y' = X + 2q - V < (B+2) q), so from an input in
 // [0,4q) the stages run 4 -> 6 -> 8 and then alternate csub(X, 4q) (8 -> 6)
@@ -250,6 +251,13 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
       }
       continue;
     }
+    // generic moduli: the same lazy schedules (the generic Montgomery product
+    // is below 2q and accepts any input below 8q, since 8q^2 < q 2^64)
+    u64 nq2 = 0 - q2, q2p1 = q2 + 1, nq4 = 0 - 2 * q2;
+    asm("" : "+s"(nq2));
+    asm("" : "+s"(q2p1));
+    asm("" : "+s"(nq4));
+    const bool red = !WIDE || wide_csub(S0 + G * LOGR + tau);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int rb = r & ((1 << GP::nb) - 1), rx = r >> GP::nb;
@@ -258,15 +266,14 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
       u64 &X = x[r];
       u64 &Y = x[r + half];
       if (!INV) {
-        const u64 uu = X >= q2 ? X - q2 : X;
+        const u64 uu = !red ? X : harvey_csub(X, WIDE ? nq4 : nq2);
         const u64 v = mont_mul<SP>(Y, w, mi);
         X = uu + v;
-        Y = uu - v + q2;
+        Y = (uu + q2p1) + ~v;
       } else {
         const u64 uu = X, vv = Y;
-        const u64 sm = uu + vv;
-        X = sm >= q2 ? sm - q2 : sm;
-        Y = mont_mul<SP>(uu - vv + q2, w, mi);
+        X = harvey_csub(uu + vv, nq2);
+        Y = mont_mul<SP>((uu + q2p1) + ~vv, w, mi);
       }
     }
   }
@@ -332,8 +339,16 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     asm("" : "+s"(nq1));
     asm("" : "+s"(nq2));
     asm("" : "+s"(nq4));
+    // EPI_COMBINE: B q + 1, so (acc + cb1) + ~v = acc + B q - v
+    u64 cb1 = (WIDE ? 2 * q2 : q2) + 1;
+    asm("" : "+s"(cb1));
     if constexpr (PG::LAST) {
-      if constexpr (!INV) {
+      if constexpr (EPI == EPI_COMBINE) {
+        // the ModDown finish takes NTT(conv) below 4q (WIDE) / 2q: one
+        // conditional subtraction instead of canonicalising (see the epilogue)
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = harvey_csub(x[r], WIDE ? nq4 : nq2);
+      } else if constexpr (!INV) {
         if (!a.lazy_out) {
 #pragma unroll
           for (int r = 0; r < R; ++r) {
@@ -367,8 +382,12 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
         const u32 kr = G0::k_reg(r);
         const u64 v = lds[lr + kr + (kr >> 4)];
         if constexpr (EPI == EPI_COMBINE) {
-          // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM
-          u64 ks = harvey_csub(mont_mul<SP>(sub_mod(pa[r], v, q), ep.pinv, mi), nq1);
+          // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM.
+          // acc - conv is formed as acc + Bq - v (v < Bq, B = 4 WIDE / 2): below
+          // 5q < 2^63 for q < 2^60 and 3q < 2^63 for q < 2^61, inside the
+          // Montgomery input bound, whose product below 1.5q (2q generic)
+          // is canonicalised by one conditional subtraction
+          u64 ks = harvey_csub(mont_mul<SP>((pa[r] + cb1) + ~v, ep.pinv, mi), nq1);
           if (ep.add) ks = add_mod(ks, pb[r], q);
           st_b(ep.out + kr, voff, ks);
         } else {
@@ -598,7 +617,7 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) ep.h[i] = i < (int)a.c_ns ? a.c_h[(size_t)i * a.c_nd + act] : 0;
   }
-  if constexpr (SP && !INV) {
+  if constexpr (!INV) {
     // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)
     if (mi.q < (1ull << 60)) {
       pass_body<LOG_N, S, LOGR, W, INV, COLS, SP, true, EPI>(a, lds, data, tw, mi, mod, w, ts, hi, gb, ep);
