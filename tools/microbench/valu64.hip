@@ -38,6 +38,7 @@ typedef uint64_t u64;
 #define B_NOT(x) asm volatile("v_not_b32 %0, %0" : "+v"(x));
 #define B_BFI(x) asm volatile("v_bfi_b32 %0, %0, %1, %0" : "+v"(x) : "v"(a));
 #define B_MOV64(x) asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
+#define B_PKMOV(x) asm volatile("v_pk_mov_b32 %0, %0, %1 op_sel:[1,1]" : "+v"(x) : "v"(k));
 #define B_SUBCO(x) asm volatile("v_sub_co_u32 %0, s[40:41], %0, %1\n v_subb_co_u32 %0, s[40:41], %0, %1, s[40:41]" : "+v"(x) : "v"(a) : "s40", "s41");
 
 KERNEL(k_lshladd, B_LSHLADD)
@@ -51,6 +52,7 @@ KERNEL32(k_subco, B_SUBCO)
 KERNEL32(k_not, B_NOT)
 KERNEL32(k_bfi, B_BFI)
 KERNEL32(k_mov, B_MOV64)
+KERNEL(k_pkmov, B_PKMOV)
 
 int main() {
   const int threads = 256, blocks = 256 * 8;
@@ -77,5 +79,6 @@ int main() {
   run("v_not_b32", k_not, 1);
   run("v_bfi_b32", k_bfi, 1);
   run("v_mov_b32", k_mov, 1);
+  run("v_pk_mov_b32 (2 dwords)", k_pkmov, 1);
   return 0;
 }
