@@ -75,9 +75,13 @@ struct fhe_ctx {
   ConvTab moddown{};           // P -> Q, h scaled by R
   // per-modulus INTT output constants for conversions fused into the next
   // NTT (CKKS, 2^15 <= N, K <= 4): P limbs N^-1 (P/p_k)^-1 R, so INTT(acc_P)
-  // emits ModDown's canonical v_k directly (ntt_fwd_combine_launch PRO_CONV)
+  // emits ModDown's canonical v_k directly (ntt_fwd_combine_launch PRO_CONV);
+  // with fuse_modup also Q limbs N^-1 (Q_j/q_i)^-1 R (q_i in digit j), so the
+  // INTT of the key-switch input emits ModUp's v_i (ntt_fwd_modup_launch)
   u64 *d_iscale = nullptr;     // [nmod]
   bool fuse_moddown = false;
+  bool fuse_modup = false;     // also alpha <= 4
+  std::vector<ConvTab> modup_tabs;  // host copies of d_modup (device pointers inside)
   std::vector<void *> blobs;   // device allocations owned by the context
   void *behz = nullptr;        // BEHZ device constants (BFV)
   // fhe_base_conv tables by (src ids, ~0, dst ids); their device arrays are
@@ -125,6 +129,11 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false,
 // the column pass (PRO_CONV); null = conv already holds the converted limbs
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro = nullptr);
+// ModUp of digit j fused into the column pass of the forward NTT of its
+// converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
+// through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
+// the lazy (< 8q) NTT outputs times R
+int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j);
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *x, u64 *e, u32 nl, u32 mod_offset, u32 n);
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);

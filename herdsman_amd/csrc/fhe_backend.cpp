@@ -262,6 +262,7 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
       tabs.push_back(make_conv_tab(c, src, dst, 2, c->fold_ninv));  // ModUp output carries a factor R
     }
     c->d_modup = (ConvTab *)ctx_upload(c, tabs.data(), sizeof(ConvTab) * tabs.size());
+    c->modup_tabs = tabs;
     std::vector<u32> src, dst;
     for (u32 k = 0; k < c->K; ++k) src.push_back(L + k);
     for (u32 i = 0; i < L; ++i) dst.push_back(i);
@@ -270,6 +271,9 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
     // ModDown fused into NTT(conv): INTT(acc_P)'s output constants carry the
     // conversion's (P/p_k)^-1 and N^-1 (two-pass sizes, at most 4 sources)
     c->fuse_moddown = c->fold_ninv && c->log_n >= 15 && c->K <= 4;
+    // ModUp fused into the column pass of the NTT of its outputs likewise
+    // (at most 4 sources per digit: the PRO_CONV prologue)
+    c->fuse_modup = c->fuse_moddown && c->alpha <= 4;
     if (c->fuse_moddown) {
       std::vector<u64> isc(c->nmod, 0);
       for (u32 k = 0; k < c->K; ++k) {
@@ -278,6 +282,15 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
         for (u32 m = 0; m < c->K; ++m)
           if (m != k) prod = hmul(prod, c->moduli[L + m] % pk, pk);
         isc[L + k] = tomont(hmul(hinv(prod, pk), hinv((u64)c->n % pk, pk), pk), pk);
+      }
+      // Q limbs: ModUp's per-source constant N^-1 (Q_j/q_i)^-1 (make_conv_tab, fold_ninv)
+      for (u32 i = 0; c->fuse_modup && i < L; ++i) {
+        const u32 lo = i / c->alpha * c->alpha, hi = std::min(lo + c->alpha, L);
+        const u64 qi = c->moduli[i];
+        u64 prod = 1;
+        for (u32 m = lo; m < hi; ++m)
+          if (m != i) prod = hmul(prod, c->moduli[m] % qi, qi);
+        isc[i] = tomont(hmul(hinv(prod, qi), hinv((u64)c->n % qi, qi), qi), qi);
       }
       c->d_iscale = (u64 *)ctx_upload(c, isc.data(), sizeof(u64) * isc.size());
       if (!c->d_iscale) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");

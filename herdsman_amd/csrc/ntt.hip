@@ -783,6 +783,41 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
   return FHE_OK;
 }
 
+// ModUp of digit j fused into the forward NTT of its converted limbs: the
+// column pass computes each target limb's conversion y_m = sum_i v_i h[i][m]
+// from the digit's source limbs v_i of dc (canonical, already scaled by the
+// INTT through d_iscale) as its prologue (PRO_CONV), so the converted limbs
+// never make an HBM round trip; the row pass leaves lazy outputs (< 8q) for
+// the inner product on special moduli, as keyswitch_run's separate NTT does.
+int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j) {
+  const u32 L = c->L, QP = c->L + c->K, N = c->n;
+  const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
+  const ConvTab &tab = c->modup_tabs[j];
+  if (c->log_n <= 14 || tab.ns > 4) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp: log_n / digit size");
+  const u32 per = 65535u;  // gridDim.y
+  for (u32 p0 = 0; p0 < n; p0 += per) {
+    const u32 np = std::min(per, n - p0);
+    NttArgs a{};
+    a.map = LimbMap{ext + ((size_t)p0 * ndig + j) * QP * N, ndig * QP, QP - (hi - lo), 0, lo, hi - lo, 0, np};
+    a.tw = c->d_tw_fwd;
+    a.mods = c->d_mods;
+    a.ninv = c->d_ninv;
+    a.log_n = c->log_n;
+    a.lazy_out = c->special;
+    a.c_src = dc + (size_t)p0 * L * N;
+    a.c_src_stride = L;
+    a.c_src_first = lo;
+    a.c_ns = tab.ns;
+    a.c_nd = tab.nd;
+    a.c_h = tab.h;
+    const u32 n_jobs = np * a.map.cnt;
+    int rc = col_pass<PRO_CONV>(c, a, false, n_jobs);
+    if (!rc) rc = row_pass(c, a, false, n_jobs);
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
 // CKKS mul+relin front end: the tensor product fused into the first pass of
 // the inverse NTT of d2 (PRO_TENSOR).  a, b, out: [n][2][L][N] (out may alias
 // a or b); dc [n][L][N] receives INTT(d2); ext's own-digit slots receive d2 R.
@@ -806,7 +841,10 @@ int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 
     t.t_QP = QP;
     t.t_alpha = c->alpha;
     t.t_ndig = ndig;
-    t.noscale = c->fold_ninv;  // dc feeds ModUp only
+    // dc feeds ModUp only: its per-source constants (N^-1 folded in) ride on
+    // this INTT when ModUp is fused into the next NTT, else N^-1 is skipped
+    if (c->fuse_modup) t.scale = c->d_iscale;
+    else t.noscale = c->fold_ninv;
     const u32 n_jobs = np * L;
     int rc;
     if (c->log_n <= 14) {
@@ -845,7 +883,8 @@ int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *d
     t.t_alpha = c->alpha;
     t.t_ndig = ndig;
     t.t_g = g & ((2u << c->log_n) - 1);
-    t.noscale = c->fold_ninv;  // dc feeds ModUp only
+    if (c->fuse_modup) t.scale = c->d_iscale;  // dc feeds ModUp only (as in ntt_inv_tensor_launch)
+    else t.noscale = c->fold_ninv;
     int rc;
     if ((rc = row_pass<PRO_AUTOMORPH>(c, t, true, np * L))) return rc;
     if ((rc = col_pass(c, t, true, np * L))) return rc;

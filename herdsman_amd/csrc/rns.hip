@@ -604,12 +604,23 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
   u64 *dc = w.dc, *ext = w.ext, *acc = w.acc, *conv = w.conv;
   int rc;
+  // CKKS at two-pass sizes: ModUp runs inside the column pass of the NTT of
+  // its outputs (ntt_fwd_modup_launch); dc then holds ModUp's scaled sources
+  const bool fused_modup = ntt_form && c->fuse_modup;
   // 1. INTT d (CKKS), unless the producer already did (ntt_inv_tensor_launch)
-  if (ntt_form && !dc_is_coef && (rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true, c->fold_ninv))) return rc;
+  if (ntt_form && !dc_is_coef &&
+      (rc = ntt_launch(c, LimbMap{dc, L, L, 0, L, 0, 0, n}, true, !fused_modup && c->fold_ninv, false,
+                       fused_modup ? c->d_iscale : nullptr)))
+    return rc;
+  if (fused_modup) {
+    // 2-3. ModUp + NTT of the converted limbs, one digit at a time
+    for (u32 j = 0; j < ndig; ++j)
+      if ((rc = ntt_fwd_modup_launch(c, dc, ext, n, ndig, j))) return rc;
+  }
   // 2. ModUp: every non-own limb of every digit
-  if ((rc = SP_DISPATCH(c, modup_impl, c, dc, L, ext, n, ndig))) return rc;
+  if (!fused_modup && (rc = SP_DISPATCH(c, modup_impl, c, dc, L, ext, n, ndig))) return rc;
   // 3. NTT the converted limbs (all limbs for BFV, whose own limbs are coefficient form)
-  for (u32 j = 0; j < ndig; ++j) {
+  for (u32 j = 0; j < ndig && !fused_modup; ++j) {
     const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
     LimbMap m{ext + (size_t)j * QP * N, ndig * QP, ntt_form ? QP - (hi - lo) : QP, 0,
               ntt_form ? lo : QP, ntt_form ? hi - lo : 0, 0, n};
