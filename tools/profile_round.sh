@@ -24,4 +24,11 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES G
   SQ_WAIT_INST_ANY SQ_WAIT_ANY --output-format csv -d "$OUT/pmc_valu" -o run -- $R > "$OUT/pmc_valu.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_LDS \
   SQ_LDS_BANK_CONFLICT --output-format csv -d "$OUT/pmc_mix" -o run -- $R > "$OUT/pmc_mix.log" 2>&1
-echo profile done
+echo profile passes done
+# 5. per-kernel PMC account of one headline wave on one stream (tools/step_pmc.py)
+S="python3 bench.py --steps 1 --warmup 1 --global-batch 128 --no-cpu --no-secondary --streams 1 --ntt-reps 1"
+timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE SQ_WAVES --output-format csv \
+  -d "$OUT/step_valu" -o run -- $S > "$OUT/step_valu.log" 2>&1
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/step_fetch" -o run -- $S > "$OUT/step_fetch.log" 2>&1
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/step_write" -o run -- $S > "$OUT/step_write.log" 2>&1
+echo step pmc done

@@ -18,14 +18,13 @@ def short(name):
 
 def load(d):
     out = collections.defaultdict(lambda: collections.defaultdict(float))
-    cnt = collections.Counter()
+    disp = collections.defaultdict(set)  # dispatches per kernel key
     for f in glob.glob(f"{d}/*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             k = (short(r["Kernel_Name"]), r["Grid_Size"])
             out[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            if r["Counter_Name"] in ("SQ_WAVES", "FETCH_SIZE", "WRITE_SIZE"):
-                cnt[k] += 1
-    return out, cnt
+            disp[k].add((f, r["Dispatch_Id"]))
+    return out, collections.Counter({k: len(v) for k, v in disp.items()})
 
 
 def main(valu_dir, fetch_dir, write_dir):
