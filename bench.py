@@ -65,6 +65,7 @@ def parse(argv=None):
     ap.add_argument("--global-batch", type=int, default=8192, help="ct-mults per step over all ranks (C5)")
     ap.add_argument("--batch", type=int, default=128, help="ct-mults per wave per GPU")
     ap.add_argument("--pool", type=int, default=1024, help="distinct resident input pairs per GPU")
+    ap.add_argument("--no-stagger", action="store_true", help="lanes start in phase (see wave_plan)")
     ap.add_argument("--streams", type=int, default=4,
                     help="contexts (one HIP stream each) that share a wave and run concurrently")
     ap.add_argument("--ntt-reps", type=int, default=20)
@@ -163,7 +164,8 @@ def main():
 
     # ---- shard of the C5 batch and its wave / pool geometry
     G = args.global_batch
-    my, B, S, waves, P, Bs, plan = wave_plan(G, args.batch, args.streams, args.pool, world, rank)
+    my, B, S, waves, P, Bs, plan = wave_plan(G, args.batch, args.streams, args.pool, world, rank,
+                                              not args.no_stagger)
     full_secondary = world == 1 and not (args.roofline_only or args.no_secondary)
 
     n = 1 << LOG_N
@@ -310,11 +312,18 @@ def main():
     return 0
 
 
-def wave_plan(G, batch, streams, pool, world, rank):
+def wave_plan(G, batch, streams, pool, world, rank, stagger=True):
     """This rank's shard of a G-ct batch (herdsman's partition rule) as waves of
     `batch` ct-mults over `streams` lanes, on a resident pool of P slots (a
     multiple of the wave).  Returns (my, B, S, waves, P, Bs, plan) with plan =
-    [(lane, lo, hi)] pool slices in issue order."""
+    [(lane, lo, hi)] pool slices in issue order.
+
+    Each lane owns P/S pool slots and a near-equal share of the shard, which it
+    runs in calls of Bs = B/S ciphertexts.  With `stagger`, lane i's first call
+    is (i+1)/S of a full one: the lanes run the same kernel sequence, so
+    without an offset their NTT passes (VALU-bound) and their conversions and
+    products (HBM-bound) would run at the same time on every stream; offset by
+    a quarter of a call each, different kernel types overlap on the GPU."""
     from herdsman_amd.dist import shard_range
 
     b0, b1 = shard_range(G, world, rank)
@@ -324,14 +333,26 @@ def wave_plan(G, batch, streams, pool, world, rank):
     waves = math.ceil(my / B) if my else 0
     P = min(max(pool // B, 1), max(waves, 1)) * B
     Bs = math.ceil(B / S)
+    PL = P // S  # pool slots per lane (>= Bs: P is a multiple of B)
+    lanes = []
+    for i in range(S):
+        l0, l1 = shard_range(my, S, i)
+        total, calls = l1 - l0, []
+        first = max(1, (Bs * (i + 1)) // S) if stagger else Bs
+        o = 0
+        while total > 0:
+            c = min(first if not calls else Bs, total)
+            if o + c > PL:
+                o = 0
+            calls.append((i, i * PL + o, i * PL + o + c))
+            o += c
+            total -= c
+        lanes.append(calls)
     plan = []
-    for w in range(waves):
-        cnt = min(B, my - w * B)
-        o = (w * B) % P
-        for i in range(S):
-            lo, hi = o + i * Bs, min(o + (i + 1) * Bs, o + cnt)
-            if lo < hi:
-                plan.append((i, lo, hi))
+    for k in range(max((len(c) for c in lanes), default=0)):
+        for calls in lanes:
+            if k < len(calls):
+                plan.append(calls[k])
     return my, B, S, waves, P, Bs, plan
 
 
