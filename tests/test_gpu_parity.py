@@ -203,17 +203,27 @@ def test_keyswitch_vs_oracle(hb, log_n, L, K, dnum):
     assert np.array_equal(hb.to_host(dout), want)
 
 
-def test_ckks_real_keys_decrypt(hb):
-    o, c = pair(hb, SCHEME_CKKS, 12, 4, 2, 2)
+@pytest.mark.parametrize("log_n,sparse", [(12, False), (16, True)])
+def test_ckks_real_keys_decrypt(hb, log_n, sparse):
+    """Real keys, decrypt, CRT: the product's error stays far below Delta^2.  At
+    N = 2^16 the whole fused pipeline runs (tensor in INTT(d2), ModUp and ModDown
+    inside the NTT column passes, the combine epilogue); the first message is
+    sparse there so the exact negacyclic reference stays cheap."""
+    o, c = pair(hb, SCHEME_CKKS, log_n, 4, 2, 2)
     Q = [int(q) for q in o.moduli[:o.L]]
     s = o.secret(3)
     s_qp = o.signed_to_rns(s, 0, o.L + o.K, ntt=True)
-    sq = np.array([[(int(x) * int(x)) % int(o.moduli[i]) for x in s_qp[i]] for i in range(o.L + o.K)],
-                  dtype=np.uint64)
+    qs = np.asarray(o.moduli[:o.L + o.K], dtype=object)[:, None]
+    sq = ((s_qp.astype(object) * s_qp.astype(object)) % qs).astype(np.uint64)
     rlk = o.switch_key(sq, s_qp, seed=4)
     rng = random.Random(5)
     delta = 1 << 30
-    u1 = [rng.randint(-4, 4) for _ in range(o.n)]
+    if sparse:
+        u1 = [0] * o.n
+        for k in rng.sample(range(o.n), 48):
+            u1[k] = rng.choice([-4, -3, -2, -1, 1, 2, 3, 4])
+    else:
+        u1 = [rng.randint(-4, 4) for _ in range(o.n)]
     u2 = [rng.randint(-4, 4) for _ in range(o.n)]
     c1 = o.encrypt(to_rns([delta * x for x in u1], Q), s_qp, 1)
     c2 = o.encrypt(to_rns([delta * x for x in u2], Q), s_qp, 2)
