@@ -375,10 +375,15 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
 }
 
 // behz_floor_to_q (oracle): fast_floor in Bsk then fastbconv_sk back to Q.
+// The third output r2 goes straight into the key-switch scratch (the KS
+// preparation of ks_prep_kernel fused here): dc = r2 and the own-digit ext
+// slot = r2 R, so r2 is not written and read back by a separate kernel.
 template <int NL, bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restrict__ eq, const u64 *__restrict__ eb,
-                                                              u64 *__restrict__ out01, u64 *__restrict__ out2,
-                                                              const BehzDev *bz, const ModInfo *mods, u32 log_n) {
+                                                              u64 *__restrict__ out01, u64 *__restrict__ dc,
+                                                              u64 *__restrict__ ext, const BehzDev *bz,
+                                                              const ModInfo *mods, u32 log_n, u32 QP, u32 dig_len,
+                                                              u32 ndig) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 ct = blockIdx.y / 3, p = blockIdx.y % 3;
   const size_t N = (size_t)1 << log_n;
@@ -415,12 +420,14 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   const u64 alpha = csub(mont_mul<SP>(sub_mod(cmsk, flsk, msk.q), bz->inv_b_msk_R, msk), msk.q);
   const bool neg = alpha > msk.q / 2;
   const u64 amag = neg ? msk.q - alpha : alpha;
-  u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : out2 + ((size_t)ct * L) * N + k;
+  u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
   for (u32 i = 0; i < L; ++i) {
     const ModInfo m = mods[i];
     const u64 cq = dot_mont<NL, SP>(w, &bz->h_b_q_R[0][i], BEHZ_MAXL, nB - 1, m);
     const u64 ab = csub(mont_mul<SP>(amag, bz->b_mod_q_R[i], m), m.q);
-    o[i * N] = neg ? add_mod(cq, ab, m.q) : sub_mod(cq, ab, m.q);
+    const u64 r = neg ? add_mod(cq, ab, m.q) : sub_mod(cq, ab, m.q);
+    o[i * N] = r;
+    if (p == 2) ext[((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k] = csub(mont_mul<SP>(r, m.r2, m), m.q);
   }
 }
 
@@ -517,12 +524,13 @@ int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xq, u64 *xb, u
 }
 
 template <bool SP>
-int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *out2, u32 n) {
+int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *dc, u64 *ext, u32 n, u32 ndig) {
   dim3 grid(c->n / EW_BLOCK, n * 3);
   const BehzDev *bz = (const BehzDev *)c->behz;
-  if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, out2, bz, c->d_mods, c->log_n);
-  else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, out2, bz, c->d_mods, c->log_n);
-  else hipLaunchKernelGGL((behz_floor_kernel<24, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, out2, bz, c->d_mods, c->log_n);
+  const u32 QP = c->L + c->K;
+  if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  else hipLaunchKernelGGL((behz_floor_kernel<24, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
   return fhe_check(c, hipGetLastError(), "behz_floor");
 }
 
@@ -753,7 +761,7 @@ int behz_setup(fhe_ctx *c) {
 
 size_t bfv_mul_ws_bytes(const fhe_ctx *c, u32 n) {
   const size_t N = c->n, L = c->L, nB = c->nB;
-  return sizeof(u64) * N * n * (4 * L + 4 * nB + 3 * L + 3 * nB + L) + keyswitch_ws_bytes(c, n);
+  return sizeof(u64) * N * n * (4 * L + 4 * nB + 3 * L + 3 * nB) + keyswitch_ws_bytes(c, n);
 }
 
 int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n) {
@@ -765,8 +773,7 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   u64 *xb = xq + (size_t)n * 4 * L * N;       // [n][4][nB][N]
   u64 *eq = xb + (size_t)n * 4 * nB * N;      // [n][3][L][N]
   u64 *eb = eq + (size_t)n * 3 * L * N;       // [n][3][nB][N]
-  u64 *r2 = eb + (size_t)n * 3 * nB * N;      // [n][L][N]
-  u64 *ksws = r2 + (size_t)n * L * N;
+  const KsWs w = ks_layout(c, n, eb + (size_t)n * 3 * nB * N);
   // 1-2. gather a0,a1,b0,b1 per item into xq and extend them to Bsk (coefficient form)
   if ((rc = SP_DISPATCH(c, behz_extend_impl, c, a, b, xq, xb, n))) return rc;
   // 3. NTT in Q and Bsk
@@ -776,8 +783,8 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   //    (unscaled: behz_floor's t constants carry N^-1)
   if ((rc = ntt_inv_bfv_tensor_launch(c, xq, eq, L, 0, n))) return rc;
   if ((rc = ntt_inv_bfv_tensor_launch(c, xb, eb, nB, bsk0, n))) return rc;
-  // 5. scale and round: r0, r1 -> out, r2 -> workspace
-  if ((rc = SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, r2, n))) return rc;
+  // 5. scale and round: r0, r1 -> out; r2 -> the key-switch scratch, prepared
+  if ((rc = SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig))) return rc;
   // 6. relinearize r2 and add to (r0, r1)
-  return keyswitch_ex(c, r2, L, rlk, out, out, n, 3u, false, ksws);
+  return keyswitch_run(c, w, rlk, out, out, n, 3u, false);
 }
