@@ -123,8 +123,9 @@ u64 host_to_mont(u64 x, u64 q);  // x * 2^64 mod q
 // NTT (ntt.hip)
 // noscale (inverse): no N^-1 multiply; lazy_out (forward): outputs below 8q, not canonical
 // scale (inverse): per-modulus output constants replacing N^-1 (d_iscale)
+// src (forward): read the input from src (same layout as m.base) instead of in place
 int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false, bool lazy_out = false,
-               const u64 *scale = nullptr);
+               const u64 *scale = nullptr, const u64 *src = nullptr);
 // pro: the ModDown conversion of acc's P limbs (scaled by d_iscale) fused into
 // the column pass (PRO_CONV); null = conv already holds the converted limbs
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
@@ -134,7 +135,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
 // the lazy (< 8q) NTT outputs times R
 int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j);
-int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *x, u64 *e, u32 nl, u32 mod_offset, u32 n);
+int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n);
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);
 // RNS kernels (rns.hip)

@@ -45,6 +45,10 @@ struct NttArgs {
   // conversion rides on the transform (fhe_ctx::d_iscale), so its outputs are
   // already the conversion's canonical v_i = [x (S/s_i)^-1]_{s_i}
   const u64 *scale;
+  // forward only: the first pass reads its limbs from src (the same layout as
+  // map.base: poly stride and limb positions) instead of transforming in
+  // place -- an out-of-place NTT, so a caller's input is never copied first
+  const u64 *src;
   // forward only: leave the outputs in the lazy range (below 8q < 2^63), for a
   // consumer whose Montgomery products accept any input below 2^63 (the KS
   // inner product on special moduli)
@@ -504,8 +508,12 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont_lazy<4, SP>(sv[j], ep.h, 1, ep.ns, mi);  // < 4q
       }
     } else {
+      // the first forward pass may read out of place (NttArgs::src)
+      const u64 *din = data;
+      if constexpr (!INV && PG::S0 == 0)
+        if (a.src) din = a.src + (data - a.map.base);
 #pragma unroll
-      for (int r = 0; r < R; ++r) x[r] = ld_d(data + ((size_t)GF::k_reg(r) << PG::LS), voff);
+      for (int r = 0; r < R; ++r) x[r] = ld_d(din + ((size_t)GF::k_reg(r) << PG::LS), voff);
     }
   }
   // the final store uses the group-0 layout for row passes and the last
@@ -593,14 +601,15 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
     ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
   }
   if constexpr (EPI == PRO_BFVT) {
-    // poly = 3 ct + e; the inputs are x[ct][4][nl][N] = (a0, a1, b0, b1)
+    // poly = 3 ct + e; the inputs are t_a, t_b [ct][2][nl][N] = (a0, a1), (b0, b1)
     const size_t LN = (size_t)a.t_L << LOG_N;
-    const u64 *x0 = a.t_a + (((size_t)(poly / 3) * 4 * a.t_L + limb) << LOG_N);
+    const size_t o = ((size_t)(poly / 3) * 2 * a.t_L + limb) << LOG_N;
+    const u64 *xa = a.t_a + o, *xb = a.t_b + o;
     ep.e = poly % 3;
-    ep.a0 = ep.e == 2 ? x0 + LN : x0;
-    ep.a1 = x0 + LN;
-    ep.b0 = ep.e == 2 ? x0 + 3 * LN : x0 + 2 * LN;
-    ep.b1 = x0 + 3 * LN;
+    ep.a0 = ep.e == 2 ? xa + LN : xa;
+    ep.a1 = xa + LN;
+    ep.b0 = ep.e == 2 ? xb + LN : xb;
+    ep.b1 = xb + LN;
   }
   if constexpr (EPI == PRO_AUTOMORPH) {
     const size_t LN = (size_t)a.t_L << LOG_N;
@@ -698,17 +707,20 @@ int row_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
 
 }  // namespace
 
-int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool lazy_out, const u64 *scale) {
+int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool lazy_out, const u64 *scale,
+               const u64 *src) {
   const u32 n_jobs = m.n_polys * m.cnt;
   if (n_jobs == 0) return FHE_OK;
+  if (inverse && src) return fhe_fail(c, FHE_ERR_INVALID, "out-of-place inverse NTT");
   if (m.n_polys > 65535u) {
     // split along polys to respect gridDim.y
     const u32 per = 65535u;
     for (u32 p0 = 0; p0 < m.n_polys; p0 += per) {
       LimbMap sub = m;
-      sub.base = m.base + (size_t)p0 * m.poly_stride * c->n;
+      const size_t off = (size_t)p0 * m.poly_stride * c->n;
+      sub.base = m.base + off;
       sub.n_polys = (m.n_polys - p0) < per ? (m.n_polys - p0) : per;
-      int rc = ntt_launch(c, sub, inverse, noscale, lazy_out, scale);
+      int rc = ntt_launch(c, sub, inverse, noscale, lazy_out, scale, src ? src + off : nullptr);
       if (rc) return rc;
     }
     return FHE_OK;
@@ -722,11 +734,13 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
   a.noscale = inverse && noscale;
   a.scale = inverse ? scale : nullptr;
   a.lazy_out = !inverse && lazy_out;
+  a.src = src;
   if (c->log_n <= 14) return single_pass(c, a, inverse, n_jobs);
   int rc;
   if (!inverse) {
     rc = col_pass(c, a, false, n_jobs);
     if (rc) return rc;
+    a.src = nullptr;  // the row pass works in place on the column pass's output
     return row_pass(c, a, false, n_jobs);
   }
   rc = row_pass(c, a, true, n_jobs);
@@ -892,12 +906,12 @@ int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *d
   return FHE_OK;
 }
 
-// BFV mul+relin: the tensor product of x [n][4][nl][N] = (a0, a1, b0, b1), NTT
-// form, in the nl-limb base starting at modulus mod_offset, fused into the
+// BFV mul+relin: the tensor product of xa = (a0, a1) and xb = (b0, b1), each
+// [n][2][nl][N] in NTT form, in the nl-limb base starting at modulus mod_offset, fused into the
 // first pass of its inverse NTT (PRO_BFVT); e [n][3][nl][N] receives the
 // coefficient-form products WITHOUT the N^-1 factor (behz_floor's constants
 // carry it).
-int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *x, u64 *e, u32 nl, u32 mod_offset, u32 n) {
+int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n) {
   const size_t N = c->n;
   const u32 per = 65535u;  // gridDim.y, a multiple of 3
   for (u32 p0 = 0; p0 < 3 * n; p0 += per) {
@@ -909,7 +923,8 @@ int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *x, u64 *e, u32 nl, u32 mod_
     t.ninv = c->d_ninv;
     t.log_n = c->log_n;
     t.noscale = 1;
-    t.t_a = x + (size_t)(p0 / 3) * 4 * nl * N;
+    t.t_a = xa + (size_t)(p0 / 3) * 2 * nl * N;
+    t.t_b = xb + (size_t)(p0 / 3) * 2 * nl * N;
     t.t_L = nl;
     const u32 n_jobs = np * nl;
     int rc;

@@ -339,17 +339,17 @@ struct BehzDev {
 // behz_extend (oracle): fastbconv_m_tilde then sm_mrq.  x [L] coef -> [nB] coef
 template <int NL, bool SP>
 // Poly p = 4 item + w of the BFV product's operands (w: a0, a1, b0, b1) is
-// read straight from the ciphertexts, copied into xq (the Q part the NTT then
-// transforms in place) and extended to Bsk in xb.
+// read straight from the ciphertexts and extended to Bsk in xb [2][n][2][nB][N]
+// (the a and b parts, each in the ciphertexts' own layout).  The Q part is not
+// copied: its forward NTT reads a and b out of place (bfv_mul_relin_impl).
 __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
-                                                               u64 *__restrict__ xq, u64 *__restrict__ xb,
-                                                               const BehzDev *bz, const ModInfo *mods, u32 log_n) {
+                                                               u64 *__restrict__ xb, const BehzDev *bz,
+                                                               const ModInfo *mods, u32 log_n, u32 n_items) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 p = blockIdx.y, item = p >> 2, w = p & 3;
   const size_t N = (size_t)1 << log_n;
   const u32 L = bz->L, nB = bz->nB;
   const u64 *s = (w < 2 ? a : b) + ((size_t)(2 * item + (w & 1)) * L) * N + k;
-  u64 *cq = xq + (size_t)p * L * N + k;
   u64 v[NL];
   u32 xmt = 0;
 #pragma unroll
@@ -358,13 +358,12 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
     if (i < (int)L) {
       const ModInfo m = mods[i];
       const u64 x = ld_nt(s + i * N);
-      cq[i * N] = x;
       v[i] = csub(mont_mul<SP>(x, bz->mt_hinv_R[i], m), m.q);
       xmt += (u32)v[i] * bz->h_mod_mt[i];
     }
   }
   const u32 r = xmt * bz->neg_inv_q_mod_mt;
-  u64 *d = xb + (size_t)p * nB * N + k;
+  u64 *d = xb + ((size_t)((w >> 1) * n_items + item) * 2 + (w & 1)) * nB * N + k;
   for (u32 j = 0; j < nB; ++j) {
     const ModInfo m = mods[bz->bsk0 + j];
     const u64 xbj = dot_mont<NL, SP>(v, &bz->h_q_bsk_R[0][j], BEHZ_MAXL + 1, L, m);
@@ -514,12 +513,12 @@ int combine_impl(fhe_ctx *c, const u64 *acc, const u64 *conv, const u64 *base, u
 }
 
 template <bool SP>
-int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xq, u64 *xb, u32 n) {
+int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
   dim3 grid(c->n / EW_BLOCK, 4 * n);
   const BehzDev *bz = (const BehzDev *)c->behz;
-  if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xq, xb, bz, c->d_mods, c->log_n);
-  else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xq, xb, bz, c->d_mods, c->log_n);
-  else hipLaunchKernelGGL((behz_extend_kernel<24, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xq, xb, bz, c->d_mods, c->log_n);
+  if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  else hipLaunchKernelGGL((behz_extend_kernel<24, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
   return fhe_check(c, hipGetLastError(), "behz_extend");
 }
 
@@ -769,20 +768,24 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   void *wsv;
   int rc = ctx_workspace(c, bfv_mul_ws_bytes(c, n), &wsv);
   if (rc) return rc;
-  u64 *xq = (u64 *)wsv;                       // [n][4][L][N]
-  u64 *xb = xq + (size_t)n * 4 * L * N;       // [n][4][nB][N]
+  u64 *xq = (u64 *)wsv;                       // [2][n][2][L][N]: NTT(a), NTT(b)
+  u64 *xb = xq + (size_t)n * 4 * L * N;       // [2][n][2][nB][N]: the Bsk extensions
   u64 *eq = xb + (size_t)n * 4 * nB * N;      // [n][3][L][N]
   u64 *eb = eq + (size_t)n * 3 * L * N;       // [n][3][nB][N]
   const KsWs w = ks_layout(c, n, eb + (size_t)n * 3 * nB * N);
-  // 1-2. gather a0,a1,b0,b1 per item into xq and extend them to Bsk (coefficient form)
-  if ((rc = SP_DISPATCH(c, behz_extend_impl, c, a, b, xq, xb, n))) return rc;
+  // 1-2. extend a0,a1,b0,b1 to Bsk (coefficient form)
+  if ((rc = SP_DISPATCH(c, behz_extend_impl, c, a, b, xb, n))) return rc;
   // 3. NTT in Q and Bsk
-  if ((rc = ntt_launch(c, LimbMap{xq, L, L, 0, L, 0, 0, 4 * n}, false))) return rc;
+  //    (the Q part out of place, straight from the ciphertexts)
+  if ((rc = ntt_launch(c, LimbMap{xq, L, L, 0, L, 0, 0, 2 * n}, false, false, false, nullptr, a))) return rc;
+  if ((rc = ntt_launch(c, LimbMap{xq + (size_t)n * 2 * L * N, L, L, 0, L, 0, 0, 2 * n}, false, false, false, nullptr,
+                       b)))
+    return rc;
   if ((rc = ntt_launch(c, LimbMap{xb, nB, nB, 0, nB, 0, bsk0, 4 * n}, false))) return rc;
   // 4. tensor in both bases, fused into the first pass of its inverse NTT
   //    (unscaled: behz_floor's t constants carry N^-1)
-  if ((rc = ntt_inv_bfv_tensor_launch(c, xq, eq, L, 0, n))) return rc;
-  if ((rc = ntt_inv_bfv_tensor_launch(c, xb, eb, nB, bsk0, n))) return rc;
+  if ((rc = ntt_inv_bfv_tensor_launch(c, xq, xq + (size_t)n * 2 * L * N, eq, L, 0, n))) return rc;
+  if ((rc = ntt_inv_bfv_tensor_launch(c, xb, xb + (size_t)n * 2 * nB * N, eb, nB, bsk0, n))) return rc;
   // 5. scale and round: r0, r1 -> out; r2 -> the key-switch scratch, prepared
   if ((rc = SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig))) return rc;
   // 6. relinearize r2 and add to (r0, r1)
