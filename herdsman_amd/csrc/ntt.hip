@@ -11,8 +11,12 @@
 // MI355X mapping.  One limb-polynomial of N u64 words is split into passes;
 // a pass owns global stages [s0, s0+S) and works on independent
 // sub-transforms of 2^S elements at stride N >> (s0+S):
-//   N <= 2^14 : ONE pass, one residue per workgroup (2^14 x 8 B = 128 KiB of
-//               LDS, 1024 threads) -- the north-star "one-residue-per-WG";
+//   N <= 2^13 : ONE pass, one residue per workgroup (up to 64 KiB of LDS) --
+//               the north-star "one-residue-per-WG"; at N = 2^14 (128 KiB, one
+//               1024-thread workgroup per CU) the fused prologue/epilogue
+//               passes keep it, while plain NTTs run two 7-stage passes with 4
+//               workgroups per CU, which measured 2% faster (C2) despite the
+//               intermediate's round trip;
 //   N  = 2^15..2^17 : two passes (column pass of stride N/2^S1, then row pass
 //               of contiguous 2^S2 blocks), because a 512 KiB N=2^16 residue
 //               exceeds the 160 KiB LDS of a CU.
@@ -686,6 +690,8 @@ int single_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
 // column pass: stages [0, S1), stride N >> S1
 template <int EPI = EPI_NONE>
 int col_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  if constexpr (EPI == EPI_NONE)
+    if (a.log_n == 14) return launch_pass<14, 7, 32, true, EPI>(c, a, inv, n_jobs);
   switch (a.log_n) {
     case 15: return launch_pass<15, 7, 32, true, EPI>(c, a, inv, n_jobs);
     case 16: return launch_pass<16, 8, 16, true, EPI>(c, a, inv, n_jobs);
@@ -697,6 +703,8 @@ int col_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
 // row pass: stages [S1, logN), contiguous blocks
 template <int EPI = EPI_NONE>
 int row_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  if constexpr (EPI == EPI_NONE)
+    if (a.log_n == 14) return launch_pass<14, 7, 32, false, EPI>(c, a, inv, n_jobs);
   switch (a.log_n) {
     case 15: return launch_pass<15, 8, 16, false, EPI>(c, a, inv, n_jobs);
     case 16: return launch_pass<16, 8, 16, false, EPI>(c, a, inv, n_jobs);
@@ -735,7 +743,10 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
   a.scale = inverse ? scale : nullptr;
   a.lazy_out = !inverse && lazy_out;
   a.src = src;
-  if (c->log_n <= 14) return single_pass(c, a, inverse, n_jobs);
+  // N = 2^14: two passes of 7 stages with 32 sub-transforms per workgroup (35 KiB
+  // of LDS, 4 workgroups per CU) instead of one pass per residue (128 KiB,
+  // one workgroup of 16 waves per CU)
+  if (c->log_n <= 13) return single_pass(c, a, inverse, n_jobs);
   int rc;
   if (!inverse) {
     rc = col_pass(c, a, false, n_jobs);
