@@ -11,7 +11,9 @@
 //         2^32, so each of the two 32-bit Montgomery rounds needs ONE
 //         v_mad_u64_u32 (m * q_hi) -- 2 multiplies in total;
 //       - generic odd moduli (explicit OpenFHE-style primes): one 64-bit round
-//         with q' = -q^-1 mod 2^64, 7 multiplies;
+//         with q' = -q^-1 mod 2^64, 7 multiplies (mont_reduce, used after the
+//         128-bit sums of the dot products); a single product uses two 32-bit
+//         CIOS rounds instead (mont_mul_gen: 8 + 2 multiplies in all);
 //   * every constant operand (twiddles, CRT constants, N^-1, P^-1) is stored
 //     pre-multiplied by R, so mont_mul(x, cR) = x * c exactly: a twiddle
 //     multiply costs 4 + 2 = 6 multiplies (Shoup needs 10);
@@ -147,10 +149,36 @@ HD void mont_mul_sp_vec(u64 (&r)[M], const u64 (&a)[M], const u64 (&b)[M], u32 q
     r[i] = (u64)(~(u32)t[i]) * q_hi + ((u64)(u32)(a[i] >> 32) * (u32)(b[i] >> 32) + (t[i] >> 32));
 }
 
+// Generic odd modulus q = q1 2^32 + q0 < 2^61: the same word-serial CIOS with
+// a 32-bit quotient digit m_k = t_k q' (q' = -q^-1 mod 2^32, the low word of
+// ModInfo::qinv_neg).  Eight v_mad_u64_u32 and two v_mul_lo_u32 (the 64-bit
+// round of mont_reduce needs 11 multiplies and a carry compare).  Each column's
+// carry out of the zeroed low word is W.hi of m_k q0 + t_k; with a1 < 2^31 and
+// b1, q1 < 2^29 every partial sum stays below 2^64.  Returns a*b*2^-64 mod q
+// in [0, 1.5q) for a < 2^63, b < q.
+HD u64 mont_mul_gen(u64 a, u64 b, const ModInfo &m) {
+  const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+  const u32 q0 = (u32)m.q, q1 = (u32)(m.q >> 32), qi = (u32)m.qinv_neg;
+  u64 P = (u64)a0 * b0;
+  OPAQUE(P);
+  const u32 m0 = (u32)P * qi;
+  u64 V = (u64)m0 * q1 + ((u64)a1 * b0 + (P >> 32));
+  OPAQUE(V);
+  V += ((u64)m0 * q0 + (u32)P) >> 32;  // (a b0 + m0 q) / 2^32
+  OPAQUE(V);
+  u64 X = (u64)a0 * b1 + V;
+  OPAQUE(X);
+  const u32 m1 = (u32)X * qi;
+  u64 Y = (u64)m1 * q1 + ((u64)a1 * b1 + (X >> 32));
+  OPAQUE(Y);
+  return Y + (((u64)m1 * q0 + (u32)X) >> 32);
+}
+
 template <bool SP>
 HD u64 mont_mul(u64 a, u64 b, const ModInfo &m) {  // a*b*2^-64, [0,2q); a < 2^63, b < q
 #if defined(__HIP_DEVICE_COMPILE__)
   if (SP) return mont_mul_sp(a, b, m.q_hi);
+  return mont_mul_gen(a, b, m);
 #endif
   return mont_reduce<SP>(mul128(a, b), m);
 }
