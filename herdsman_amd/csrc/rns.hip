@@ -174,8 +174,9 @@ __global__ void __launch_bounds__(EW_BLOCK) modup_kernel(const u64 *__restrict__
   conv_store<NS, SP, CONV_CPT, true>(sh, v, t.ns, t.nd, ext + ((size_t)(ct * ndig + j) * QP) * N + k, N, true, 0);
 }
 
-// KS preparation for an input d (fhe_keyswitch, BFV): dc = d and the own-digit
-// slot of ext = d * R.  (mul_relin / rotate fuse this into tensor / automorph.)
+// KS preparation for an input d (fhe_keyswitch): dc = d and the own-digit
+// slot of ext = d * R.  (mul_relin / rotate fuse this into the tensor INTT /
+// automorphism prologues, BFV mul_relin into the BEHZ floor.)
 template <bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) ks_prep_kernel(const u64 *__restrict__ d, u32 d_stride,
                                                            u64 *__restrict__ dc, u64 *__restrict__ ext,
@@ -603,7 +604,7 @@ static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
 }
 
 // Hybrid key switching on a PREPARED scratch (dc and the own-digit limbs of
-// ext filled by ks_prep / the tensor INTT prologue / automorph_ks).
+// ext filled by ks_prep / the tensor INTT prologue / automorph_ks / the BEHZ floor).
 //   out : [n][2][L][N], out_b = (add_mask bit b ? base_b : 0) + KS(d)_b;
 //         base may alias out (element-wise).
 static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
