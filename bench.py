@@ -274,6 +274,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not (args.no_cpu or args.roofline_only):
         cpu = run_cpu_baseline(args)
+        if "digest_2ct" in cpu:
+            cpu["gpu_bitexact_2ct"] = gpu_digest_2ct(hb, ctx, dev) == cpu["digest_2ct"]
 
     if rank == 0:
         line = {
@@ -490,6 +492,23 @@ def _host_cores():
     return cores, aff, quota, model
 
 
+def gpu_digest_2ct(hb, ctx, dev):
+    """SHA-256 of the GPU's first two products of the CPU baseline's sample (the
+    same SplitMix64 seeds, generated on the device): equal to the child's digest
+    iff the two outputs agree bit for bit."""
+    import hashlib
+
+    import torch
+    n = 1 << LOG_N
+    a = ctx.fill_uniform(hb.empty((2, 2, L, n), device=dev), seed=1)
+    b = ctx.fill_uniform(hb.empty((2, 2, L, n), device=dev), seed=2)
+    k = ctx.fill_uniform(hb.empty(ctx.key_shape(), device=dev), seed=3)
+    out = hb.empty((2, 2, L, n), device=dev)
+    ctx.mul_relin(a, b, k, out)
+    torch.cuda.synchronize(dev)
+    return hashlib.sha256(hb.to_host(out).tobytes()).hexdigest()
+
+
 def run_cpu_baseline(args):
     """The oracle in a child process (no GPU, no torch) so that its OpenMP threads
     can be pinned (OMP_PROC_BIND / OMP_PLACES are read when libgomp starts)."""
@@ -509,6 +528,10 @@ def run_cpu_baseline(args):
 
 def cpu_baseline_child(args):
     """CPU oracle (test infrastructure) on bounded samples of the bench workloads."""
+    import hashlib
+
+    import numpy as np
+
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_ffi import Oracle, SCHEME_BFV, SCHEME_CKKS
 
@@ -535,6 +558,9 @@ def cpu_baseline_child(args):
         "kind": "port",
         "sample": f"{done} CKKS ct-mult+relin at N=2^16 L=12 K=4 dnum=3 in {dt:.1f} s "
                   f"(batches of {threads}, OpenMP one ciphertext per thread)",
+        # the CPU and GPU outputs of the same inputs are compared in
+        # the same run; the GPU side recomputes the first two products (main())
+        "digest_2ct": hashlib.sha256(np.ascontiguousarray(o.mul_relin(a[:2], b[:2], k)).tobytes()).hexdigest(),
     }
     sec = {}
     g = o.galois_elt(1)
