@@ -599,6 +599,28 @@ def test_bfv_mul_relin_fused_tensor_sizes(hb, log_n, L, K, dnum):
     assert np.array_equal(hb.to_host(da), want)
 
 
+def test_generic_moduli_metric_size(hb):
+    """OpenFHE-style primes at the metric parameters (N=2^16, L=12, K=4, dnum=3;
+    60-bit Q on the wide lazy schedule, 61-bit P on the narrow one): the fused
+    mul+relin pipeline on the generic 32-bit CIOS Montgomery product, edge
+    values (0, 1, q-1) included, and an NTT round trip of edge values."""
+    log_n, L, K, dnum = 16, 12, 4, 3
+    mods = np.array(_generic_primes(60, log_n, L) + _generic_primes(61, log_n, K), dtype=np.uint64)
+    o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum, moduli=mods)
+    a = _edge_inputs(o, (1, 2, L, 1 << log_n), seed=180)
+    b = _edge_inputs(o, (1, 2, L, 1 << log_n), seed=181)
+    k = o.uniform(o.key_shape(), seed=182)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(k), dout)
+    assert np.array_equal(hb.to_host(dout), o.mul_relin(a, b, k))
+    x = _edge_inputs(o, (2, L + K, 1 << log_n), seed=183)
+    d = hb.to_device(x)
+    c.ntt_fwd(d)
+    assert np.array_equal(hb.to_host(d), o.ntt_fwd(x.copy()))
+    c.ntt_inv(d)
+    assert np.array_equal(hb.to_host(d), x)
+
+
 def test_generic_moduli_two_pass_fused_paths(hb):
     """Generic (non 2^32) moduli at a two-pass size: the CKKS tensor and
     automorphism prologues and the unscaled inverse NTTs on the generic
