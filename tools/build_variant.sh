@@ -3,6 +3,7 @@
 # patched copy of csrc (for A/B runs: HERD_FHE_LIB=herdsman_amd/var/<name>/libherdsman_fhe.so).
 #   tools/build_variant.sh NAME [sed-expression FILE]...
 #   REV=<git rev> tools/build_variant.sh NAME ...   (csrc taken from that revision)
+#   EXTRA='<hipcc flags>' tools/build_variant.sh NAME  (extra flags for the .hip translation units)
 set -e
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -15,7 +16,7 @@ fi
 sed -i "s@\"../../include/plugins/fhe_backend.h\"@\"plugins/fhe_backend.h\"@" "$D"/csrc/*.hpp "$D"/csrc/*.cpp "$D"/csrc/*.hip
 while [ $# -ge 2 ]; do sed -i "$1" "$D/csrc/$2"; shift 2; done
 cd "$D"
-for f in ntt rns; do /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" -c -o $f.o csrc/$f.hip & done
+for f in ntt rns; do /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" $EXTRA -c -o $f.o csrc/$f.hip & done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" -x hip -c -o be.o csrc/fhe_backend.cpp &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o libherdsman_fhe.so ntt.o rns.o be.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
