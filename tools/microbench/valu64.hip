@@ -28,6 +28,15 @@ typedef uint64_t u64;
     out[blockIdx.x * blockDim.x + threadIdx.x] = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7 ^ k;  \
   }
 
+#define KERNELF(name, BODY)                                                       \
+  __global__ void name(u64 *out, u64 seed) {                                     \
+    double x0 = 1.0 + threadIdx.x * 1e-3 + seed * 1e-9, x1 = x0 * 1.1, x2 = x0 * 1.2, x3 = x0 * 1.3; \
+    double x4 = x0 * 1.4, x5 = x0 * 1.5, x6 = x0 * 1.6, x7 = x0 * 1.7;           \
+    double k = 0.9999999;                                                        \
+    for (int i = 0; i < ITER; ++i) { BODY(x0) BODY(x1) BODY(x2) BODY(x3) BODY(x4) BODY(x5) BODY(x6) BODY(x7) } \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (u64)(x0 + x1 + x2 + x3 + x4 + x5 + x6 + x7); \
+  }
+
 #define B_LSHLADD(x) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(x) : "v"(k));
 #define B_MAD(x) asm volatile("v_mad_u64_u32 %0, s[40:41], %1, %1, %0" : "+v"(x) : "v"(a) : "s40", "s41");
 #define B_ADDC(x) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(x) : "v"(a) : "vcc");
@@ -41,6 +50,14 @@ typedef uint64_t u64;
 #define B_PKMOV(x) asm volatile("v_pk_mov_b32 %0, %0, %1 op_sel:[1,1]" : "+v"(x) : "v"(k));
 #define B_SUBCO(x) asm volatile("v_sub_co_u32 %0, s[40:41], %0, %1\n v_subb_co_u32 %0, s[40:41], %0, %1, s[40:41]" : "+v"(x) : "v"(a) : "s40", "s41");
 
+#define B_FMAF64(x) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(x) : "v"(k));
+#define B_MULF64(x) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(x) : "v"(k));
+#define B_ADDF64(x) asm volatile("v_add_f64 %0, %0, %1" : "+v"(x) : "v"(k));
+#define B_RNDF64(x) asm volatile("v_rndne_f64 %0, %0" : "+v"(x));
+KERNELF(k_fmaf64, B_FMAF64)
+KERNELF(k_mulf64, B_MULF64)
+KERNELF(k_addf64, B_ADDF64)
+KERNELF(k_rndf64, B_RNDF64)
 KERNEL(k_lshladd, B_LSHLADD)
 KERNEL(k_mad, B_MAD)
 KERNEL32(k_addc, B_ADDC)
@@ -80,5 +97,9 @@ int main() {
   run("v_bfi_b32", k_bfi, 1);
   run("v_mov_b32", k_mov, 1);
   run("v_pk_mov_b32 (2 dwords)", k_pkmov, 1);
+  run("v_fma_f64", k_fmaf64, 1);
+  run("v_mul_f64", k_mulf64, 1);
+  run("v_add_f64", k_addf64, 1);
+  run("v_rndne_f64", k_rndf64, 1);
   return 0;
 }
