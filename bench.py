@@ -115,15 +115,28 @@ def launch(args) -> int:
 
 
 def _rccl_comm(dev):
-    """ncclComm_t of PyTorch's RCCL process group on `dev` (0 if unavailable): the
+    """(ncclComm_t of PyTorch's RCCL process group on `dev`, error text): the
     backend's fhe_bcast_key must use a communicator of the librccl instance it
-    is bound to, which in a torch process is torch's own."""
+    is bound to, which in a torch process is torch's own.
+    A failed hand-off is returned as an error string, never swallowed: the
+    bench line reports it (key_bcast_error) and stderr says so."""
     import torch.distributed as dist
     try:
         be = dist.group.WORLD._get_backend(dev)
-        return int(be._comm_ptr()) if hasattr(be, "_comm_ptr") else 0
-    except Exception:
-        return 0
+        if not hasattr(be, "_comm_ptr"):
+            return 0, f"{type(be).__name__} has no _comm_ptr (torch {__import__('torch').__version__})"
+        comm = int(be._comm_ptr())
+        return comm, None if comm else "_comm_ptr() returned 0"
+    except Exception as e:  # reported, not hidden
+        return 0, f"{type(e).__name__}: {e}"
+
+
+def _key_digest(key, dev):
+    """Per-rank checksum of the key words (a torch reduction on the device), so
+    the line can state that every rank holds the same key after the broadcast."""
+    import torch
+    w = key.view(torch.int64)
+    return int(torch.bitwise_xor(w[0::2], w[1::2]).sum().item()) & ((1 << 64) - 1)
 
 
 # -------------------------------------------------------------------- ranks
@@ -186,20 +199,30 @@ def main():
     if rank == 0:
         ctx.fill_uniform(rlk, seed=0x524C4B)
     torch.cuda.synchronize(dev)
-    bcast = "none (1 rank)"
+    bcast, bcast_err, key_ok = "none (1 rank)", None, True
     if world > 1:
         dist.barrier()
     t_b = time.perf_counter()
     if world > 1:
-        comm = _rccl_comm(dev) if backend == "nccl" else 0
+        comm, bcast_err = _rccl_comm(dev) if backend == "nccl" else (0, None)
         if comm:
             ctx.bcast_key(rlk, comm, root=0)  # fhe_bcast_key: ncclBroadcast over xGMI
             bcast = "fhe_bcast_key (RCCL)"
         else:
+            if bcast_err:
+                print(f"bench.py: RCCL communicator hand-off failed ({bcast_err}); "
+                      "broadcasting the key through torch.distributed instead", file=sys.stderr, flush=True)
             broadcast_key(rlk, src=0)
             bcast = f"torch.distributed.broadcast ({backend})"
     torch.cuda.synchronize(dev)
     key_bcast_ms = (time.perf_counter() - t_b) * 1e3
+    if world > 1:
+        digests = [None] * world
+        dist.all_gather_object(digests, _key_digest(rlk, dev))
+        key_ok = len(set(digests)) == 1
+        if not key_ok:
+            print(f"bench.py: key digests differ across ranks after the broadcast: {digests}", file=sys.stderr)
+            return 3
 
     a = hb.empty((P, 2, L, n), device=dev)
     b = hb.empty((P, 2, L, n), device=dev)
@@ -304,6 +327,8 @@ def main():
             "per_rank_ct_mult_per_s": [round(v, 1) for v in per_rank],
             "key_bcast_ms": round(key_bcast_ms, 3),
             "key_bcast_via": bcast,
+            "key_bcast_error": bcast_err,
+            "key_identical_on_all_ranks": key_ok,
             "algorithmic_GBps_ct_mult": round(value / n_gpus * 6 * L * n * 8 / 1e9, 1),
             "cpu_baseline": cpu,
             "secondary": secondary,
@@ -376,13 +401,16 @@ def dry_run(args):
     t0 = time.perf_counter()
     time.sleep(0.01 * (rank + 1))
     elapsed = max_over_ranks(time.perf_counter() - t0)
-    shards = [(rank, my, covered, os.getpid())]
+    shards = [(rank, my, covered, os.getpid(), local)]
     if world > 1:
         shards = [None] * world
-        dist.all_gather_object(shards, (rank, my, covered, os.getpid()))
+        dist.all_gather_object(shards, (rank, my, covered, os.getpid(), local))
+    per_rank = [s[1] / elapsed if elapsed > 0 else 0.0 for s in sorted(shards)]
     if rank == 0:
         print(json.dumps({"dry_run": True, "ranks": world, "shards": shards, "wave": B, "waves": waves,
-                          "pool": P, "lanes": S, "elapsed": elapsed}), flush=True)
+                          "pool": P, "lanes": S, "elapsed": elapsed, "steps": args.steps, "warmup": args.warmup,
+                          "n_gpus": len({s[4] for s in shards}), "per_rank_ct_mult_per_s": per_rank,
+                          "value": args.global_batch / elapsed if elapsed > 0 else 0.0}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
@@ -400,6 +428,9 @@ def profile_fields(path, limbs, algo_per_limb):
     if per_limb:
         res["traffic"] = round(per_limb * limbs)
         res["traffic_per_limb_ntt"] = round(per_limb)
+        # not measured in this run: the PMC bytes per limb-NTT of the committed
+        # rocprofv3 passes (FETCH_SIZE x2 + WRITE_SIZE) times this call's limbs
+        res["traffic_source"] = f"{os.path.relpath(path, ROOT)} (rocprofv3 --pmc, committed)"
     launch_ns, plimbs = pj.get("ntt_fwd_launch_ns"), pj.get("limbs_per_launch")
     if launch_ns and plimbs:
         res["rocprof_launch_ms"] = round(launch_ns / 1e6, 4)

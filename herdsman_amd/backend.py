@@ -62,6 +62,8 @@ SIGNATURES = {
     "fhe_memcpy_h2d_async": (C.c_int, [_vp, _vp, _vp, _sz]),
     "fhe_memcpy_d2h_async": (C.c_int, [_vp, _vp, _vp, _sz]),
     "fhe_use_own_stream": (C.c_int, [_vp]),
+    "fhe_mark": (C.c_int, [_vp, C.c_uint32]),
+    "fhe_wait_mark": (C.c_int, [_vp, C.c_uint32]),
     "fhe_ntt_fwd": (C.c_int, [_vp, _vp, _u32, _u32, _u32]),
     "fhe_ntt_inv": (C.c_int, [_vp, _vp, _u32, _u32, _u32]),
     "fhe_poly_add": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32, _u32]),
@@ -102,7 +104,10 @@ def load_library():
     if not os.path.exists(path):
         raise FheBackendError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = C.CDLL(path)
+    variant = bool(os.environ.get("HERD_FHE_LIB"))
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue  # an older build under A/B may predate an entry point it is not asked for
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
     _lib = lib

@@ -90,6 +90,8 @@ struct fhe_ctx {
   // scratch
   void *ws = nullptr;
   size_t ws_bytes = 0;
+  // fhe_mark / fhe_wait_mark events, created on first use
+  hipEvent_t marks[FHE_MAX_MARKS] = {};
 };
 
 // Binds the context's device for the duration of an ABI call and restores the
@@ -106,6 +108,20 @@ struct DeviceBind {
   }
   DeviceBind(const DeviceBind &) = delete;
   DeviceBind &operator=(const DeviceBind &) = delete;
+};
+
+// The same for a bare device id (context creation and destruction).
+struct DeviceIdBind {
+  int prev = -1;
+  explicit DeviceIdBind(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~DeviceIdBind() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceIdBind(const DeviceIdBind &) = delete;
+  DeviceIdBind &operator=(const DeviceIdBind &) = delete;
 };
 
 // helpers shared by the translation units (fhe_backend.cpp)
@@ -128,8 +144,11 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false,
                const u64 *scale = nullptr, const u64 *src = nullptr);
 // pro: the ModDown conversion of acc's P limbs (scaled by d_iscale) fused into
 // the column pass (PRO_CONV); null = conv already holds the converted limbs
+// ext / ksk: acc's Q limbs are the key-switching inner product of ext [n][ndig][QP][N]
+// with ksk [ndig][2][QP][N], formed in the last pass instead of read (EPI_KSQ)
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
-                           u64 *out, u32 add_mask, const ConvTab *pro = nullptr);
+                           u64 *out, u32 add_mask, const ConvTab *pro = nullptr, const u64 *ext = nullptr,
+                           const u64 *ksk = nullptr, u32 ndig = 0);
 // ModUp of digit j fused into the column pass of the forward NTT of its
 // converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive

@@ -169,6 +169,10 @@ static void ctx_release(fhe_ctx *c) {
   c->ws = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   c->own_stream = nullptr;
+  for (hipEvent_t &e : c->marks) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
 }
 
 // ------------------------------------------------------------ context
@@ -316,7 +320,7 @@ int fhe_ctx_create(const fhe_params *params, int device, fhe_ctx **out) {
     return FHE_ERR_DEVICE;
   }
   if (device < 0 || device >= ndev) return FHE_ERR_INVALID;
-  if (hipSetDevice(device) != hipSuccess) return FHE_ERR_DEVICE;
+  DeviceIdBind bind(device);  // the caller's current device is restored on return
   fhe_ctx *c = new (std::nothrow) fhe_ctx();
   if (!c) return FHE_ERR_OOM;
   c->device = device;
@@ -333,7 +337,7 @@ int fhe_ctx_create(const fhe_params *params, int device, fhe_ctx **out) {
 
 void fhe_ctx_destroy(fhe_ctx *c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  DeviceIdBind bind(c->device);
   (void)hipStreamSynchronize(c->stream);
   ctx_release(c);
   delete c;
@@ -358,6 +362,24 @@ int fhe_synchronize(fhe_ctx *c) {
   if (!c) return FHE_ERR_INVALID;
   DeviceBind bind(c);
   return fhe_check(c, hipStreamSynchronize(c->stream), "synchronize");
+}
+
+int fhe_mark(fhe_ctx *c, uint32_t slot) {
+  if (!c) return FHE_ERR_INVALID;
+  if (slot >= FHE_MAX_MARKS) return fhe_fail(c, FHE_ERR_INVALID, "mark slot out of range");
+  DeviceBind bind(c);
+  if (!c->marks[slot]) {
+    int rc = fhe_check(c, hipEventCreateWithFlags(&c->marks[slot], hipEventDisableTiming), "mark create");
+    if (rc) return rc;
+  }
+  return fhe_check(c, hipEventRecord(c->marks[slot], c->stream), "mark record");
+}
+
+int fhe_wait_mark(fhe_ctx *c, uint32_t slot) {
+  if (!c) return FHE_ERR_INVALID;
+  if (slot >= FHE_MAX_MARKS || !c->marks[slot]) return fhe_fail(c, FHE_ERR_INVALID, "wait on an unrecorded mark");
+  DeviceBind bind(c);
+  return fhe_check(c, hipEventSynchronize(c->marks[slot]), "mark wait");
 }
 
 int fhe_reserve(fhe_ctx *c, uint32_t max_batch) {

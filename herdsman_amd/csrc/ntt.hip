@@ -65,6 +65,11 @@ struct NttArgs {
   const u64 *e_pinv;     // [L] P^-1 R mod q_i
   u32 e_acc_stride;
   u32 e_add_mask;
+  // EPI_KSQ (EPI_COMBINE whose acc_Q is the key-switching inner product, formed
+  // here instead of being read): acc[p][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1,
+  // p = 2 ct + b, with ext [ct][e_ndig][e_QP][N] and ksk [e_ndig][2][e_QP][N]
+  const u64 *e_ext, *e_ksk;
+  u32 e_ndig, e_QP;
   // PRO_TENSOR (first pass of the inverse NTT of d2 in CKKS mul+relin, poly =
   // ciphertext): the pass reads the operands a, b [ct][2][L][N] instead of d2,
   // writes the relinearisation base out[ct][0] = a0 b0, out[ct][1] = a0 b1 + a1 b0
@@ -94,11 +99,18 @@ struct NttArgs {
 // product e = (a0 b0, a0 b1 + a1 b0, a1 b1) in one RNS base
 // PRO_CONV: prologue of a forward first (column) pass, the base conversion
 // that produces its input
-enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, PRO_CONV = 5 };
+// EPI_KSQ + d - 1: EPI_COMBINE with the Q limbs' key-switching inner product
+// over d = 1..4 digits fused in (the digit count is compile-time)
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, PRO_CONV = 5, EPI_KSQ = 6 };
+__host__ __device__ constexpr bool is_ksq(int e) { return e >= EPI_KSQ && e < EPI_KSQ + 4; }
+__host__ __device__ constexpr int ksq_digits(int e) { return e - EPI_KSQ + 1; }
+__host__ __device__ constexpr bool is_combine(int e) { return e == EPI_COMBINE || is_ksq(e); }
 
 // per-workgroup epilogue / prologue operands (resolved once per limb)
 struct EpiRow {
   const u64 *acc;
+  const u64 *kext, *kksk;  // EPI_KSQ: digit 0's ext / key row of this limb (digit j at + j stride)
+  size_t ext_j, ksk_j;     // digit strides (words)
   const u64 *base;
   u64 *out;
   u64 pinv;
@@ -329,12 +341,12 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     // EPI_COMBINE: the epilogue's acc and base words are in flight while the
     // last group computes (the LDS footprint caps occupancy at 4 waves per
     // SIMD, so the 128-VGPR budget has room for them)
-    constexpr int RE = EPI == EPI_COMBINE ? R : 1;
+    constexpr int RE = is_combine(EPI) ? R : 1;
     u64 pa[RE], pb[RE];
-    if constexpr (EPI == EPI_COMBINE) {
+    if constexpr (is_combine(EPI)) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        pa[r] = ld_b(ep.acc + Grp<S, LOGR, 0>::k_reg(r), voff);
+        if constexpr (EPI == EPI_COMBINE) pa[r] = ld_b(ep.acc + Grp<S, LOGR, 0>::k_reg(r), voff);
         pb[r] = ep.add ? ld_b(ep.base + Grp<S, LOGR, 0>::k_reg(r), voff) : 0;
       }
     }
@@ -351,7 +363,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     u64 cb1 = (WIDE ? 2 * q2 : q2) + 1;
     asm("" : "+s"(cb1));
     if constexpr (PG::LAST) {
-      if constexpr (EPI == EPI_COMBINE) {
+      if constexpr (is_combine(EPI)) {
         // the ModDown finish takes NTT(conv) below 4q (WIDE) / 2q: one
         // conditional subtraction instead of canonicalising (see the epilogue)
 #pragma unroll
@@ -389,13 +401,47 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
       for (int r = 0; r < R; ++r) {
         const u32 kr = G0::k_reg(r);
         const u64 v = lds[lr + kr + (kr >> 4)];
-        if constexpr (EPI == EPI_COMBINE) {
+        if constexpr (is_combine(EPI)) {
           // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM.
           // acc - conv is formed as acc + Bq - v (v < Bq, B = 4 WIDE / 2): below
           // 5q < 2^63 for q < 2^60 and 3q < 2^63 for q < 2^61, inside the
           // Montgomery input bound, whose product below 1.5q (2q generic)
           // is canonicalised by one conditional subtraction
-          u64 ks = harvey_csub(mont_mul<SP>((pa[r] + cb1) + ~v, ep.pinv, mi), nq1);
+          u64 acc;
+          if constexpr (is_ksq(EPI)) {
+            // acc_Q = sum_j ext_j ksk_j R^-1 (ext carries R), at the store
+            // position: acc_Q never makes an HBM round trip.  Each product is
+            // below 1.5q (2q generic), so one subtraction of 4q (WIDE) leaves
+            // the lazy sum below 4q; otherwise it is made canonical.
+            constexpr int KD = ksq_digits(EPI);
+            u64 e[KD], k[KD], pr[KD];
+#pragma unroll
+            for (int j = 0; j < KD; ++j) {
+              e[j] = ld_b(ep.kext + j * ep.ext_j + kr, voff);
+              k[j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
+            }
+            if constexpr (SP) {
+              mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+            } else {
+#pragma unroll
+              for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
+            }
+            acc = pr[0];
+            if constexpr (WIDE) {
+              // q < 2^60: the whole sum stays below 6q < 2^63
+#pragma unroll
+              for (int j = 1; j < KD; ++j) acc += pr[j];
+              if constexpr (KD > 2) acc = harvey_csub(acc, nq4);
+            } else {
+              // q < 2^61: keep the running sum below 2q, then canonical
+#pragma unroll
+              for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
+              acc = harvey_csub(acc, nq1);
+            }
+          } else {
+            acc = pa[r];
+          }
+          u64 ks = harvey_csub(mont_mul<SP>((acc + cb1) + ~v, ep.pinv, mi), nq1);
           if (ep.add) ks = add_mod(ks, pb[r], q);
           st_b(ep.out + kr, voff, ks);
         } else {
@@ -403,7 +449,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
         }
       }
     } else {
-      static_assert(EPI != EPI_COMBINE, "epilogues run in the re-laid-out row store");
+      static_assert(!is_combine(EPI), "epilogues run in the re-laid-out row store");
       // column pass (or single pass ending in group 0): element k of this
       // thread sits at voff + k_reg(r) << LS -- a compile-time offset on the
       // scalar base, so the address costs no VALU
@@ -531,17 +577,25 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
   group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, 0>(x, tc, lds, tw, data, voff, w, ts, hi, a, mi, mod, ep);
 }
 
-template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI>
-__global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
-  static_assert(EPI == EPI_COMBINE || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
+#ifndef NTT_MINW
+#define NTT_MINW 1
+#endif
+// WM (forward passes): the lazy schedule of the launch's moduli, chosen on the
+// host (wide_mode): 1 all WIDE (q < 2^60), 0 all narrow, 2 mixed (a per-
+// workgroup branch between both; the kernel then carries both code paths and
+// needs ~150 VGPRs instead of ~90, i.e. 3 waves per SIMD instead of the 4 the
+// LDS allows: a launch over one modulus class avoids it)
+template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int WM>
+__global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NTT_MINW : 1) ntt_pass(NttArgs a) {
+  static_assert(is_combine(EPI) || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
                     EPI == PRO_BFVT || EPI == PRO_CONV,
                 "ntt_pass epilogues");
   static_assert(EPI != PRO_CONV || (!INV && COLS), "the conversion prologue feeds a forward column pass");
-  static_assert(EPI != EPI_COMBINE || (!INV && !COLS), "epilogues follow a forward row pass");
+  static_assert(!is_combine(EPI) || (!INV && !COLS), "epilogues follow a forward row pass");
   static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT) || (INV && !COLS),
                 "prologues feed an inverse row pass");
   using PG = PassGeo<LOG_N, S, COLS, INV>;
-  static_assert(EPI != EPI_COMBINE || PG::LAST, "epilogues run in the last pass");
+  static_assert(!is_combine(EPI) || PG::LAST, "epilogues run in the last pass");
   constexpr int T = 1 << (S - LOGR);
   static_assert(LOGR == 4, "register tile is 16 words");
   extern __shared__ u64 lds[];
@@ -551,6 +605,32 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   // scalar base (global_load ... saddr): no 64-bit VALU address arithmetic
   const u32 tid = threadIdx.x;
   u32 bx = blockIdx.x, poly = blockIdx.y, act = blockIdx.z;
+  if constexpr (EPI == EPI_NONE) {
+    // every block of one job (poly, limb) on ONE XCD (ids are dealt
+    // round-robin over the 8 XCDs), jobs still in dispatch order: the blocks'
+    // row segments of one residue meet in one L2 (forward launch 2.07 ->
+    // 2.01 ms, profiles/r03/ab_xcd_job.txt)
+    const u32 nj = gridDim.y * gridDim.z;
+    if ((nj & 7) == 0) {
+      const u32 lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+      const u32 r = lin >> 3;
+      bx = r % gridDim.x;
+      const u32 j = (r / gridDim.x) * 8 + (lin & 7);
+      poly = j % gridDim.y;
+      act = j / gridDim.y;
+    }
+  }
+  if constexpr (is_ksq(EPI)) {
+    // the 2 n polys (ct, b) of one (limb, row block) on consecutive workgroup
+    // ids of ONE XCD: the limb's key rows (2 dnum of them) stay in that XCD's
+    // L2 for the whole batch, and the b = 1 item re-reads the ext rows the
+    // b = 0 item just fetched
+    const u32 np = gridDim.y, lin = blockIdx.x + gridDim.x * (blockIdx.y + np * blockIdx.z);
+    const u32 r = lin >> 3, g = (r / np) * 8 + (lin & 7);  // g = (limb, row block)
+    poly = r % np;
+    bx = g % gridDim.x;
+    act = g / gridDim.x;
+  }
   if constexpr (EPI == PRO_CONV) {
     // the T target limbs of one source block (poly, column block) run on
     // consecutive workgroup ids of ONE XCD (ids are dealt round-robin over the
@@ -586,7 +666,14 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
   const u32 gb = (hi << (S + PG::LS)) + (u & (stride - 1));
 
   EpiRow ep{};
-  if constexpr (EPI == EPI_COMBINE) {
+  if constexpr (is_combine(EPI)) {
+    if constexpr (is_ksq(EPI)) {
+      const size_t N = (size_t)1 << LOG_N;
+      ep.ext_j = (size_t)a.e_QP * N;
+      ep.ksk_j = 2 * ep.ext_j;
+      ep.kext = a.e_ext + ((size_t)(poly >> 1) * a.e_ndig * a.e_QP + limb) * N;
+      ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_QP + limb) * N;
+    }
     ep.acc = a.e_acc + (((size_t)poly * a.e_acc_stride + limb) << LOG_N);
     ep.base = a.e_base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
     ep.out = a.e_out + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
@@ -630,17 +717,27 @@ __global__ void __launch_bounds__(W << (S - LOGR)) ntt_pass(NttArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) ep.h[i] = i < (int)a.c_ns ? a.c_h[(size_t)i * a.c_nd + act] : 0;
   }
-  if constexpr (!INV) {
+  if constexpr (!INV && WM == 2) {
     // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)
     if (mi.q < (1ull << 60)) {
       pass_body<LOG_N, S, LOGR, W, INV, COLS, SP, true, EPI>(a, lds, data, tw, mi, mod, w, ts, hi, gb, ep);
       return;
     }
   }
-  pass_body<LOG_N, S, LOGR, W, INV, COLS, SP, false, EPI>(a, lds, data, tw, mi, mod, w, ts, hi, gb, ep);
+  pass_body<LOG_N, S, LOGR, W, INV, COLS, SP, !INV && WM == 1, EPI>(a, lds, data, tw, mi, mod, w, ts, hi, gb, ep);
 }
 
-template <int LOG_N, int S, int W, bool COLS, bool INV, bool SP, int EPI>
+// lazy-schedule class of the moduli a launch over map m touches (ntt_pass WM)
+int wide_mode(const fhe_ctx *c, const LimbMap &m) {
+  bool wide = false, narrow = false;
+  for (u32 act = 0; act < m.cnt; ++act) {
+    const u64 q = c->moduli[m.mod_offset + limbmap_limb(m, act)];
+    (q < (1ull << 60) ? wide : narrow) = true;
+  }
+  return wide && narrow ? 2 : wide ? 1 : 0;
+}
+
+template <int LOG_N, int S, int W, bool COLS, bool INV, bool SP, int EPI, int WM = 0>
 int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   constexpr int LOGR = 4;
   constexpr int NT = W << (S - LOGR);
@@ -649,18 +746,28 @@ int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   // dispatch order: row blocks, then polys, then limbs -- the resident
   // workgroups share one modulus, so its twiddle table stays in L2
   dim3 grid(subs / W, n_jobs / a.map.cnt, a.map.cnt);
-  auto k = ntt_pass<LOG_N, S, LOGR, W, INV, COLS, SP, EPI>;
+  auto k = ntt_pass<LOG_N, S, LOGR, W, INV, COLS, SP, EPI, WM>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);
   return fhe_check(c, hipGetLastError(), "ntt_pass launch");
 }
 
+// a forward pass, with the lazy schedule class of its moduli
+template <int LOG_N, int S, int W, bool COLS, int EPI, bool SP>
+int launch_fwd(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
+  switch (wide_mode(c, a.map)) {
+    case 1: return launch_one<LOG_N, S, W, COLS, false, SP, EPI, 1>(c, a, n_jobs);
+    case 0: return launch_one<LOG_N, S, W, COLS, false, SP, EPI, 0>(c, a, n_jobs);
+  }
+  return launch_one<LOG_N, S, W, COLS, false, SP, EPI, 2>(c, a, n_jobs);
+}
+
 template <int LOG_N, int S, int W, bool COLS, int EPI = EPI_NONE>
 int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
-  if constexpr (EPI == EPI_COMBINE || EPI == PRO_CONV) {
+  if constexpr (is_combine(EPI) || EPI == PRO_CONV) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
-    return c->special ? launch_one<LOG_N, S, W, COLS, false, true, EPI>(c, a, n_jobs)
-                      : launch_one<LOG_N, S, W, COLS, false, false, EPI>(c, a, n_jobs);
+    return c->special ? launch_fwd<LOG_N, S, W, COLS, EPI, true>(c, a, n_jobs)
+                      : launch_fwd<LOG_N, S, W, COLS, EPI, false>(c, a, n_jobs);
   } else if constexpr (EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH || EPI == PRO_BFVT) {
     if (!inv) return fhe_fail(c, FHE_ERR_INVALID, "prologue on a forward pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
@@ -668,9 +775,9 @@ int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
   } else {
     if (c->special)
       return inv ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
-                 : launch_one<LOG_N, S, W, COLS, false, true, EPI>(c, a, n_jobs);
+                 : launch_fwd<LOG_N, S, W, COLS, EPI, true>(c, a, n_jobs);
     return inv ? launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs)
-               : launch_one<LOG_N, S, W, COLS, false, false, EPI>(c, a, n_jobs);
+               : launch_fwd<LOG_N, S, W, COLS, EPI, false>(c, a, n_jobs);
   }
 }
 
@@ -763,11 +870,15 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
 // the ModDown finish fused into its last pass (EPI_COMBINE):
 //   out[p][i] = (add_mask bit (p & 1) ? base[p][i] : 0) + (acc[p][i] - NTT(conv)[p][i]) P^-1  mod q_i
 // conv is transformed in place by the first pass only; acc rows have stride acc_stride limbs.
+// With ext (EPI_KSQ, two-pass sizes) acc's Q limbs are not read: the last pass
+// forms acc[2 ct + b][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1 itself.
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
-                           u64 *out, u32 add_mask, const ConvTab *pro) {
-  const u32 L = c->L;
+                           u64 *out, u32 add_mask, const ConvTab *pro, const u64 *ext, const u64 *ksk, u32 ndig) {
+  const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
-  const u32 per = 65535u;  // gridDim.y
+  if (ext && (c->log_n <= 14 || ndig > 4 || (n_polys & 1)))
+    return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch inner product: log_n / digits");
+  const u32 per = 65534u;  // gridDim.y, even (the polys of a ciphertext stay together)
   for (u32 p0 = 0; p0 < n_polys; p0 += per) {
     const u32 np = std::min(per, n_polys - p0);
     NttArgs a{};
@@ -782,6 +893,12 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
     a.e_pinv = c->d_pinv;
     a.e_acc_stride = acc_stride;
     a.e_add_mask = add_mask;
+    if (ext) {
+      a.e_ext = ext + (size_t)(p0 / 2) * ndig * QP * N;
+      a.e_ksk = ksk;
+      a.e_ndig = ndig;
+      a.e_QP = QP;
+    }
     const u32 n_jobs = np * L;
     int rc;
     if (c->log_n <= 14) {
@@ -801,7 +918,13 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
         rc = col_pass(c, a, false, n_jobs);
       }
       if (rc) return rc;
-      rc = row_pass<EPI_COMBINE>(c, a, false, n_jobs);
+      switch (ext ? ndig : 0) {
+        case 1: rc = row_pass<EPI_KSQ>(c, a, false, n_jobs); break;
+        case 2: rc = row_pass<EPI_KSQ + 1>(c, a, false, n_jobs); break;
+        case 3: rc = row_pass<EPI_KSQ + 2>(c, a, false, n_jobs); break;
+        case 4: rc = row_pass<EPI_KSQ + 3>(c, a, false, n_jobs); break;
+        default: rc = row_pass<EPI_COMBINE>(c, a, false, n_jobs);
+      }
     }
     if (rc) return rc;
   }
@@ -837,7 +960,19 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
     a.c_h = tab.h;
     const u32 n_jobs = np * a.map.cnt;
     int rc = col_pass<PRO_CONV>(c, a, false, n_jobs);
-    if (!rc) rc = row_pass(c, a, false, n_jobs);
+    if (rc) return rc;
+    // the row pass as one launch per modulus class where that splits the
+    // targets into a Q part and a P part of one class each (ntt_pass WM)
+    NttArgs aq = a, ap = a;
+    aq.map = LimbMap{a.map.base, a.map.poly_stride, L - (hi - lo), 0, lo, hi - lo, 0, np};
+    ap.map = LimbMap{a.map.base, a.map.poly_stride, c->K, L, c->K, 0, 0, np};
+    const int wq = wide_mode(c, aq.map), wp = wide_mode(c, ap.map);
+    if (wq != 2 && wp != 2 && wq != wp && aq.map.cnt && ap.map.cnt) {
+      if ((rc = row_pass(c, aq, false, np * aq.map.cnt))) return rc;
+      rc = row_pass(c, ap, false, np * ap.map.cnt);
+    } else {
+      rc = row_pass(c, a, false, n_jobs);
+    }
     if (rc) return rc;
   }
   return FHE_OK;

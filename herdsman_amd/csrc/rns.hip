@@ -201,9 +201,9 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_prep_kernel(const u64 *__restrict
 template <bool SP, int MAXD>
 __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restrict__ ext, const u64 *__restrict__ ksk,
                                                             u64 *__restrict__ acc, const ModInfo *mods, u32 QP,
-                                                            u32 ndig, u32 n_ct, u32 log_n) {
+                                                            u32 ndig, u32 n_ct, u32 log_n, u32 limb0) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const u32 i = blockIdx.y;
+  const u32 i = limb0 + blockIdx.y;
   const size_t N = (size_t)1 << log_n;
   const ModInfo m = mods[i];
   const size_t ext_ct = (size_t)ndig * QP * N, acc_ct = (size_t)2 * QP * N;
@@ -466,18 +466,19 @@ int modup_impl(fhe_ctx *c, const u64 *dc, u32 dcs, u64 *ext, u32 n, u32 ndig) {
   return fhe_check(c, hipGetLastError(), "modup_kernel");
 }
 
+// limbs [limb0, limb0 + nl) of Q u P
 template <bool SP>
-int inner_impl(fhe_ctx *c, const u64 *ext, const u64 *ksk, u64 *acc, u32 n, u32 ndig) {
+int inner_impl(fhe_ctx *c, const u64 *ext, const u64 *ksk, u64 *acc, u32 n, u32 ndig, u32 limb0, u32 nl) {
   const u32 QP = c->L + c->K;
-  dim3 grid(c->n / EW_BLOCK, QP);
+  dim3 grid(c->n / EW_BLOCK, nl);
   if (ndig <= 4)
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 4>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 4>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0);
   else if (ndig <= 8)
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 8>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 8>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0);
   else if (ndig <= 16)
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 16>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 16>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0);
   else
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 0>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 0>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0);
   return fhe_check(c, hipGetLastError(), "ks_inner_kernel");
 }
 
@@ -636,15 +637,20 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
     // (< 8q) NTT outputs as they are, so the last pass skips canonicalising
     if ((rc = ntt_launch(c, m, false, false, c->special))) return rc;
   }
-  // 4. inner product with the key
-  if ((rc = SP_DISPATCH(c, inner_impl, c, ext, ksk, acc, n, ndig))) return rc;
+  // 4. inner product with the key.  With the fused ModDown and at most 4
+  //    digits, the Q limbs' inner product runs inside the last pass of
+  //    NTT(conv) (EPI_KSQ), so only the P limbs (ModDown's sources) are formed
+  //    here: acc_Q is never written and read back
+  const bool ksq = ntt_form && c->fuse_moddown && ndig <= 4;
+  if ((rc = SP_DISPATCH(c, inner_impl, c, ext, ksk, acc, n, ndig, ksq ? L : 0, ksq ? K : QP))) return rc;
   // 5-6. ModDown for NTT-form results: INTT the P part with the conversion's
   //      source constants as its output scale, then NTT(conv) with the P -> Q
   //      conversion in its first pass and the combine in its last
   //      (out = base + (acc_Q - conv) P^-1): conv never makes an HBM round trip
   if (ntt_form && c->fuse_moddown) {
     if ((rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale))) return rc;
-    return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, &c->moddown);
+    return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, &c->moddown, ksq ? ext : nullptr,
+                                  ksk, ndig);
   }
   // 5. ModDown: INTT the P part (all of Q u P for BFV), convert P -> Q
   if ((rc = ntt_launch(c, LimbMap{acc, QP, ntt_form ? K : QP, ntt_form ? L : 0, QP, 0, 0, 2 * n}, true,

@@ -73,12 +73,37 @@ class PartitionView {
   std::vector<std::pair<const uint8_t *, uint32_t>> rows_;
 };
 
+// A partition file read with pread: the row index (payload offsets and
+// lengths) is built once from the u32 length prefixes, and a caller reads any
+// byte range of a row straight into its own memory (the worker's pinned
+// staging buffers: one copy from the page cache, no mapping).  Throws on a
+// missing file, a truncated row or a short read.
+class PartitionIndex {
+ public:
+  explicit PartitionIndex(const std::filesystem::path &path);
+  ~PartitionIndex();
+  PartitionIndex(const PartitionIndex &) = delete;
+  PartitionIndex &operator=(const PartitionIndex &) = delete;
+  size_t size() const { return rows_.size(); }
+  uint32_t row_len(size_t i) const { return rows_[i].second; }
+  // bytes [off, off + len) of row i's payload -> dst
+  void read(size_t i, size_t off, void *dst, size_t len) const;
+
+ private:
+  std::filesystem::path path_;
+  int fd_ = -1;
+  std::vector<std::pair<uint64_t, uint32_t>> rows_;  // payload file offset, length
+};
+
 // Output partition written through a temporary file renamed into place by
 // commit(): a task that fails half-way leaves no output behind.  Rows are
 // gathered with writev from caller memory (header + words), no staging copy.
+// Like herdsman's own partition writes (storage_service.cpp), this protects
+// against failures of the process; `durable` adds fsync of the file before
+// the rename and of the directory after it, for a crash of the machine.
 class PartitionWriter {
  public:
-  explicit PartitionWriter(const std::filesystem::path &path);
+  explicit PartitionWriter(const std::filesystem::path &path, bool durable = false);
   ~PartitionWriter();
   PartitionWriter(const PartitionWriter &) = delete;
   PartitionWriter &operator=(const PartitionWriter &) = delete;
@@ -89,7 +114,7 @@ class PartitionWriter {
  private:
   std::filesystem::path path_, tmp_;
   int fd_ = -1;
-  bool done_ = false;
+  bool done_ = false, durable_ = false;
 };
 
 }  // namespace herdsman_gpu

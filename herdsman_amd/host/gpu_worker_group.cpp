@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <stdexcept>
@@ -96,7 +97,51 @@ PartitionView::~PartitionView() {
   if (map_) ::munmap(map_, bytes_);
 }
 
-PartitionWriter::PartitionWriter(const std::filesystem::path &path) : path_(path) {
+PartitionIndex::PartitionIndex(const std::filesystem::path &path) : path_(path) {
+  fd_ = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd_ < 0) throw std::runtime_error("cannot open partition " + path.string());
+  struct stat st {};
+  if (::fstat(fd_, &st) != 0) {
+    ::close(fd_);
+    throw std::runtime_error("cannot stat partition " + path.string());
+  }
+  (void)::posix_fadvise(fd_, 0, 0, POSIX_FADV_SEQUENTIAL);
+  const uint64_t size = (uint64_t)st.st_size;
+  uint64_t pos = 0;
+  while (pos < size) {
+    uint32_t len = 0;
+    if (size - pos < 4 || ::pread(fd_, &len, 4, (off_t)pos) != 4) {
+      ::close(fd_);
+      throw std::runtime_error("truncated row header in " + path.string());
+    }
+    if (size - pos - 4 < len) {
+      ::close(fd_);
+      throw std::runtime_error("truncated row in " + path.string());
+    }
+    rows_.emplace_back(pos + 4, len);
+    pos += 4 + (uint64_t)len;
+  }
+}
+
+PartitionIndex::~PartitionIndex() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+void PartitionIndex::read(size_t i, size_t off, void *dst, size_t len) const {
+  if (off + len > rows_[i].second) throw std::runtime_error("row holds fewer ciphertexts than the circuit reads");
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  uint64_t at = rows_[i].first + off;
+  while (len) {
+    const ssize_t r = ::pread(fd_, d, len, (off_t)at);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) throw std::runtime_error("short read from " + path_.string());
+    d += r;
+    at += (uint64_t)r;
+    len -= (size_t)r;
+  }
+}
+
+PartitionWriter::PartitionWriter(const std::filesystem::path &path, bool durable) : path_(path), durable_(durable) {
   std::filesystem::create_directories(path.parent_path());
   tmp_ = path;
   tmp_ += ".tmp-" + std::to_string((unsigned long)::getpid()) + "-" +
@@ -139,6 +184,7 @@ void PartitionWriter::append(const std::vector<std::pair<const void *, size_t>> 
 }
 
 void PartitionWriter::commit() {
+  if (durable_ && ::fsync(fd_) != 0) throw std::runtime_error("fsync failed " + tmp_.string());
   if (::close(fd_) != 0) {
     fd_ = -1;
     throw std::runtime_error("close failed " + tmp_.string());
@@ -146,6 +192,13 @@ void PartitionWriter::commit() {
   fd_ = -1;
   std::filesystem::rename(tmp_, path_);
   done_ = true;
+  if (durable_) {
+    const int dfd = ::open(path_.parent_path().c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    if (dfd >= 0) {
+      (void)::fsync(dfd);
+      ::close(dfd);
+    }
+  }
 }
 
 // ------------------------------------------------------------- device state
@@ -270,13 +323,25 @@ struct Pinned {
   }
 };
 
+// Pinned staging of one batch in flight: one input buffer per PUSH_INPUT and
+// the output buffer; a lane alternates between two of them, so batch k+1's
+// inputs are read and batch k-1's outputs written while batch k runs.
+struct Slot {
+  std::vector<std::unique_ptr<Pinned>> in;
+  Pinned out;
+  size_t r0 = 0, n = 0;
+};
+
 // one lane's state for one schema: context (own stream), buffers, staging
 struct LaneSchema {
   SchemaCtx s;
   std::unique_ptr<Arena> arena;
-  std::vector<std::unique_ptr<Pinned>> in_stage;  // one per PUSH_INPUT of a batch
-  Pinned out_stage;
+  Slot slot[2];
 };
+
+double secs_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
 
 }  // namespace
 
@@ -304,6 +369,10 @@ struct GpuWorkerGroup::Device {
 
 GpuWorkerGroup::GpuWorkerGroup(GpuWorkerGroupConfig config) : config_(std::move(config)) {
   if (config_.devices.empty()) throw std::invalid_argument("GpuWorkerGroup needs at least one device");
+  if (!circuits_lowerable())
+    std::fprintf(stderr,
+                 "GpuWorkerGroup: herd_common's Circuit has no lowering to backend ops (INTEGRATION.md §2); "
+                 "every task will complete with ERROR\n");
   if (config_.lanes_per_device == 0) config_.lanes_per_device = 1;
   if (config_.max_batch == 0) config_.max_batch = 1;
   for (int d : config_.devices) {
@@ -335,9 +404,11 @@ GpuWorkerGroup::~GpuWorkerGroup() {
       for (auto &kv : l->schemas) {
         LaneSchema &ls = *kv.second;
         ls.arena.reset();
-        ls.in_stage.clear();
-        if (ls.out_stage.p) fhe_host_free(ls.out_stage.ctx, ls.out_stage.p);
-        ls.out_stage.p = nullptr;
+        for (Slot &sl : ls.slot) {
+          sl.in.clear();
+          if (sl.out.p) fhe_host_free(sl.out.ctx, sl.out.p);
+          sl.out.p = nullptr;
+        }
         fhe_ctx_destroy(ls.s.ctx);
       }
       l->schemas.clear();
@@ -351,13 +422,23 @@ GpuWorkerGroup::~GpuWorkerGroup() {
   completion_thread_.join();
 }
 
+StageStats GpuWorkerGroup::stage_stats() {
+  std::lock_guard lk(stats_m_);
+  return stats_;
+}
+
+void GpuWorkerGroup::reset_stage_stats() {
+  std::lock_guard lk(stats_m_);
+  stats_ = StageStats{};
+}
+
 std::size_t GpuWorkerGroup::concurrent_workers() const noexcept {
   return devices_.size() * config_.lanes_per_device;
 }
 
 std::shared_ptr<IWorkerGroup::TaskHandle> GpuWorkerGroup::schedule_task(const herd::common::task_t &task) {
   auto h = std::make_shared<Handle>();
-  if (std::holds_alternative<std::monostate>(task)) {
+  if (std::holds_alternative<std::monostate>(task) || !circuits_lowerable()) {
     complete(h, Status::ERROR);  // delivered once the executor attaches its callback
     return h;
   }
@@ -441,6 +522,12 @@ std::vector<Instr> lower_circuit(const C &c) {
   }
 }
 
+template <class C>
+constexpr bool lowerable_v = requires(const C &c) {
+  c.program.begin()->op;
+  c.program.begin()->arg;
+};
+
 template <class T>
 int schema_id(T v) {
   return static_cast<int>(v);  // herd_common's SchemaType is an enum (key_service.cpp:28)
@@ -514,17 +601,10 @@ std::shared_ptr<KeySet> device_keys(std::mutex &m, std::map<std::pair<std::strin
   return k;
 }
 
-// parse ciphertext k of a row
-// words of ciphertext k of a row (unaligned in the file: the caller memcpys them)
-const uint8_t *row_ct(const SchemaCtx &s, const uint8_t *row, uint32_t len, uint32_t k) {
-  const size_t one = sizeof(CtHeader) + s.ct_words() * 8;
-  if (len < (k + 1) * one) throw std::runtime_error("row holds fewer ciphertexts than the circuit reads");
-  CtHeader h;
-  std::memcpy(&h, row + k * one, sizeof(h));
+void check_ct_header(const SchemaCtx &s, const CtHeader &h) {
   if (h.magic != kCtMagic || h.version != 1 || h.scheme != s.scheme || h.log_n != s.log_n || h.n_limbs != s.L ||
       h.moduli_digest != s.q_digest)
     throw std::runtime_error("ciphertext header does not match the schema context");
-  return row + k * one + sizeof(CtHeader);
 }
 
 CtHeader ct_header(const SchemaCtx &s) {
@@ -544,23 +624,34 @@ const DevBuf &galois_key(const SchemaCtx &s, const KeySet &ks, int32_t steps, ui
   return it->second;
 }
 
-// Evaluate the program on `n` rows at once.  Every input is staged into its
-// own pinned buffer and copied asynchronously, so the host gathers input k+1
-// while input k is on the wire and earlier kernels run; the batch ends with
-// one asynchronous copy back and one synchronisation.
-void eval_map_batch(LaneSchema &ls, const KeySet &ks, const std::vector<Instr> &prog, const PartitionView &rows,
-                    size_t r0, size_t n, PartitionWriter &out) {
+// Batch k of a MapTask, first half: read the rows' ciphertexts straight from
+// the partition file into slot k % 2's pinned buffers (pread), then enqueue
+// H2D, the program's ops and D2H on the lane's stream and mark the slot.
+// Nothing waits for the GPU here.
+void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vector<Instr> &prog,
+                       const PartitionIndex &rows, size_t r0, size_t n, StageStats &st) {
   const SchemaCtx &s = ls.s;
-  const size_t cw = s.ct_words();
+  Slot &sl = ls.slot[si];
+  sl.r0 = r0;
+  sl.n = n;
+  const size_t cw = s.ct_words(), one = sizeof(CtHeader) + cw * 8;
   std::vector<ArenaBuf> stack;
   size_t push = 0;
+  double read_s = 0;
+  const auto t_enq = std::chrono::steady_clock::now();
   for (const auto &ins : prog) {
     switch (ins.op) {
       case Op::PUSH_INPUT: {
-        if (ls.in_stage.size() <= push) ls.in_stage.push_back(std::make_unique<Pinned>());
-        uint64_t *host = reinterpret_cast<uint64_t *>(ls.in_stage[push++]->reserve(s.ctx, cw * n * 8));
-        for (size_t r = 0; r < n; ++r)
-          std::memcpy(host + r * cw, row_ct(s, rows.row(r0 + r), rows.row_len(r0 + r), ins.arg), cw * 8);
+        if (sl.in.size() <= push) sl.in.push_back(std::make_unique<Pinned>());
+        uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[push++]->reserve(s.ctx, cw * n * 8));
+        const auto t_r = std::chrono::steady_clock::now();
+        for (size_t r = 0; r < n; ++r) {
+          CtHeader h;
+          rows.read(r0 + r, (size_t)ins.arg * one, &h, sizeof(h));
+          check_ct_header(s, h);
+          rows.read(r0 + r, (size_t)ins.arg * one + sizeof(h), host + r * cw, cw * 8);
+        }
+        read_s += secs_since(t_r);
         ArenaBuf d(*ls.arena, cw * n);
         ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, d.p, host, cw * n * 8), "h2d");
         stack.push_back(std::move(d));
@@ -598,11 +689,31 @@ void eval_map_batch(LaneSchema &ls, const KeySet &ks, const std::vector<Instr> &
     }
   }
   if (stack.size() != 1) throw std::runtime_error("circuit must leave exactly one ciphertext");
-  uint64_t *host = reinterpret_cast<uint64_t *>(ls.out_stage.reserve(s.ctx, cw * n * 8));
+  uint64_t *host = reinterpret_cast<uint64_t *>(sl.out.reserve(s.ctx, cw * n * 8));
   ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, host, stack.back().p, cw * n * 8), "d2h");
-  ck(s.ctx, fhe_synchronize(s.ctx), "batch sync");  // staging buffers are free again after this
+  // the device buffers go back to the arena now: later ops that reuse them are
+  // ordered after this batch's copies by the stream
+  ck(s.ctx, fhe_mark(s.ctx, (uint32_t)si), "mark");
+  st.read_s += read_s;
+  st.enqueue_s += secs_since(t_enq) - read_s;
+}
+
+// Second half: wait for the slot's mark (its D2H has landed, its H2D sources
+// are free again) and append the batch's rows to the output partition.
+void finish_map_batch(LaneSchema &ls, int si, PartitionWriter &out, StageStats &st) {
+  const SchemaCtx &s = ls.s;
+  Slot &sl = ls.slot[si];
+  auto t0 = std::chrono::steady_clock::now();
+  ck(s.ctx, fhe_wait_mark(s.ctx, (uint32_t)si), "batch wait");
+  st.wait_s += secs_since(t0);
+  t0 = std::chrono::steady_clock::now();
+  const size_t cw = s.ct_words();
+  const uint64_t *host = reinterpret_cast<const uint64_t *>(sl.out.p);
   const CtHeader h = ct_header(s);
-  for (size_t r = 0; r < n; ++r) out.append({{&h, sizeof(h)}, {host + r * cw, cw * 8}});
+  for (size_t r = 0; r < sl.n; ++r) out.append({{&h, sizeof(h)}, {host + r * cw, cw * 8}});
+  st.write_s += secs_since(t0);
+  st.batches += 1;
+  st.rows += sl.n;
 }
 
 std::filesystem::path frame_path(const std::filesystem::path &root, const herd::common::UUID &session,
@@ -611,6 +722,8 @@ std::filesystem::path frame_path(const std::filesystem::path &root, const herd::
 }
 
 }  // namespace
+
+bool GpuWorkerGroup::circuits_lowerable() noexcept { return lowerable_v<herd::common::Circuit>; }
 
 void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
   while (true) {
@@ -623,19 +736,31 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
       dev.queue.pop_front();
     }
     Status st = Status::COMPLETED;
+    LaneSchema *cur = nullptr;
+    StageStats stats;
     try {
       if (std::holds_alternative<herd::common::MapTask>(job.task)) {
         const auto &t = std::get<herd::common::MapTask>(job.task);
         const int schema = schema_id(t.crypto_key_ptr.schema_type);
         const std::vector<Instr> prog = lower_circuit(t.circuit);
         LaneSchema &ls = lane_schema(lane.schemas, config_, dev.id, schema);
+        cur = &ls;
         auto ks = device_keys(dev.keys_m, dev.keys, ls.s, config_.key_dir, t.session_uuid.as_string(), schema);
-        const PartitionView rows(frame_path(config_.storage_dir, t.session_uuid, t.input_data_frame_ptr.pointer));
-        PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr));
-        for (size_t r0 = 0; r0 < rows.size(); r0 += config_.max_batch) {
+        const PartitionIndex rows(frame_path(config_.storage_dir, t.session_uuid, t.input_data_frame_ptr.pointer));
+        PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr),
+                            config_.durable_outputs);
+        // two-deep software pipeline over the batches: enqueue batch k, then
+        // write batch k-1 while batch k runs on the GPU, then read batch k+1
+        int pending = -1;  // slot of the batch enqueued but not yet written
+        size_t k = 0;
+        for (size_t r0 = 0; r0 < rows.size(); r0 += config_.max_batch, ++k) {
           const size_t n = std::min<size_t>(config_.max_batch, rows.size() - r0);
-          eval_map_batch(ls, *ks, prog, rows, r0, n, out);
+          const int si = (int)(k & 1);
+          enqueue_map_batch(ls, si, *ks, prog, rows, r0, n, stats);
+          if (pending >= 0) finish_map_batch(ls, pending, out, stats);
+          pending = si;
         }
+        if (pending >= 0) finish_map_batch(ls, pending, out, stats);
         out.commit();
       } else {
         // ReduceTask: combine every row of every input partition into one
@@ -645,39 +770,53 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         const int schema = schema_id(t.crypto_key_ptr.schema_type);
         const std::vector<Instr> prog = lower_circuit(t.circuit);
         LaneSchema &ls = lane_schema(lane.schemas, config_, dev.id, schema);
+        cur = &ls;
         const SchemaCtx &s = ls.s;
         const bool mul = !prog.empty() && prog.front().op == Op::MUL_RELIN;
         std::shared_ptr<KeySet> ks;
         if (mul) ks = device_keys(dev.keys_m, dev.keys, s, config_.key_dir, t.session_uuid.as_string(), schema);
-        std::vector<std::unique_ptr<PartitionView>> parts;
+        std::vector<std::unique_ptr<PartitionIndex>> parts;
         size_t count = 0;
         for (const auto &in : t.input_data_frame_ptrs) {
-          parts.push_back(std::make_unique<PartitionView>(frame_path(config_.storage_dir, t.session_uuid, in.pointer)));
+          parts.push_back(std::make_unique<PartitionIndex>(frame_path(config_.storage_dir, t.session_uuid, in.pointer)));
           count += parts.back()->size();
         }
         if (count == 0) throw std::runtime_error("reduce over no rows");
         const size_t cw = s.ct_words();
-        if (ls.in_stage.empty()) ls.in_stage.push_back(std::make_unique<Pinned>());
-        uint64_t *host = reinterpret_cast<uint64_t *>(ls.in_stage[0]->reserve(s.ctx, count * cw * 8));
+        Slot &sl = ls.slot[0];
+        if (sl.in.empty()) sl.in.push_back(std::make_unique<Pinned>());
+        uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[0]->reserve(s.ctx, count * cw * 8));
         size_t r = 0;
         for (const auto &pv : parts)
-          for (size_t i = 0; i < pv->size(); ++i, ++r)
-            std::memcpy(host + r * cw, row_ct(s, pv->row(i), pv->row_len(i), 0), cw * 8);
+          for (size_t i = 0; i < pv->size(); ++i, ++r) {
+            CtHeader h;
+            pv->read(i, 0, &h, sizeof(h));
+            check_ct_header(s, h);
+            pv->read(i, sizeof(h), host + r * cw, cw * 8);
+          }
         ArenaBuf a(*ls.arena, count * cw);
         ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, a.p, host, count * cw * 8), "h2d");
         // balanced tree, one batched add / mul+relin per level (fhe_reduce)
         ck(s.ctx, fhe_reduce(s.ctx, a.p, (uint32_t)count, mul ? FHE_REDUCE_MUL_RELIN : FHE_REDUCE_ADD,
                              mul ? ks->relin.p : nullptr, a.p), "reduce");
-        uint64_t *res = reinterpret_cast<uint64_t *>(ls.out_stage.reserve(s.ctx, cw * 8));
+        uint64_t *res = reinterpret_cast<uint64_t *>(sl.out.reserve(s.ctx, cw * 8));
         ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, res, a.p, cw * 8), "d2h");
         ck(s.ctx, fhe_synchronize(s.ctx), "reduce sync");
-        PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr));
+        PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr),
+                            config_.durable_outputs);
         const CtHeader h = ct_header(s);
         out.append({{&h, sizeof(h)}, {res, cw * 8}});
         out.commit();
       }
     } catch (const std::exception &) {
       st = Status::ERROR;  // no exception crosses the seam (executor.cpp:168-178 fails the job)
+      // copies of this task may still be reading or filling the lane's pinned
+      // buffers: let them finish before the next task reuses (or regrows) them
+      if (cur) (void)fhe_synchronize(cur->s.ctx);
+    }
+    {
+      std::lock_guard lk(stats_m_);
+      stats_ += stats;
     }
     complete(job.handle, st);
   }

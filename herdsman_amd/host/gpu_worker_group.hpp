@@ -61,6 +61,24 @@ inline std::vector<SchemaParams> default_schemas() {
   return {ckks, bfv};
 }
 
+// Where a lane's time goes over MapTasks (wg_run bench prints it): reading
+// rows into pinned memory, enqueueing copies and kernels, waiting for a batch's
+// GPU work (copies both ways + kernels, after the overlap with the host work),
+// writing output rows.
+struct StageStats {
+  double read_s = 0, enqueue_s = 0, wait_s = 0, write_s = 0;
+  uint64_t batches = 0, rows = 0;
+  StageStats &operator+=(const StageStats &o) {
+    read_s += o.read_s;
+    enqueue_s += o.enqueue_s;
+    wait_s += o.wait_s;
+    write_s += o.write_s;
+    batches += o.batches;
+    rows += o.rows;
+    return *this;
+  }
+};
+
 struct GpuWorkerGroupConfig {
   std::vector<int> devices{0};
   std::filesystem::path storage_dir;  // <storage>/<session>/<frame>/<partition>
@@ -68,6 +86,7 @@ struct GpuWorkerGroupConfig {
   std::vector<SchemaParams> schemas = default_schemas();
   uint32_t lanes_per_device = 4;      // concurrent tasks per device (context + stream each)
   uint32_t max_batch = 64;            // rows per batched GPU call
+  bool durable_outputs = false;       // fsync output partitions (PartitionWriter)
 };
 
 class GpuWorkerGroup : public IWorkerGroup {
@@ -77,6 +96,12 @@ class GpuWorkerGroup : public IWorkerGroup {
 
   std::shared_ptr<TaskHandle> schedule_task(const herd::common::task_t &task) override;
   std::size_t concurrent_workers() const noexcept override;
+  // summed over the lanes since construction / the last reset (not part of the seam)
+  StageStats stage_stats();
+  void reset_stage_stats();
+  // false when herd_common's Circuit has no lowering to the backend's ops
+  // (under HERDSMAN_REAL_SEAM): the group then fails every task at once
+  static bool circuits_lowerable() noexcept;
 
   class Handle;
 
@@ -98,6 +123,8 @@ class GpuWorkerGroup : public IWorkerGroup {
   std::deque<std::shared_ptr<Handle>> done_;
   bool stopping_ = false;
   std::thread completion_thread_;
+  std::mutex stats_m_;
+  StageStats stats_;
 };
 
 class GpuWorkerGroup::Handle : public IWorkerGroup::TaskHandle {

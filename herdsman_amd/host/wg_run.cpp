@@ -6,13 +6,15 @@
 //   wg_run map    STORAGE KEYS SESSION SCHEMA PARAMS IN_FRAME PART OUT_FRAME PROGRAM...
 //   wg_run reduce STORAGE KEYS SESSION SCHEMA PARAMS OUT_FRAME OUT_PART IN_FRAME:PART... [-- mul]
 //   wg_run race   N            (seam test: N malformed tasks, callback attached late)
-//   wg_run bench  DIR PARAMS PARTS ROWS [LANES [MAX_BATCH]]
+//   wg_run bench  DIR PARAMS PARTS ROWS [LANES [MAX_BATCH [REPS]]]
 //                 MapTask throughput: writes PARTS partitions of ROWS rows
 //                 (two ciphertexts each, uniform residues made on the GPU) and a
 //                 relinearisation key under DIR, then keeps concurrent_workers()
 //                 MapTasks "in0 in1 mul" in flight, as the Executor does
 //                 (executor.cpp:96-113), and reports ct-mult+relin/s end to end
-//                 (partition read, PCIe both ways, GPU, partition write).
+//                 (partition read, PCIe both ways, GPU, partition write): the
+//                 mean and spread of REPS (default 5) warm repetitions after one
+//                 warm-up, and where the lanes' time went (GpuWorkerGroup::stage_stats).
 // PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file]   PROGRAM tokens: in<i> add sub mul rot:<k>
 #include <algorithm>
 #include <chrono>
@@ -98,7 +100,7 @@ static void ckb(fhe_ctx *c, int rc, const char *what) {
 }
 
 static int bench(int argc, char **argv) {
-  if (argc < 6) throw std::runtime_error("usage: wg_run bench DIR PARAMS PARTS ROWS [LANES [MAX_BATCH]]");
+  if (argc < 6) throw std::runtime_error("usage: wg_run bench DIR PARAMS PARTS ROWS [LANES [MAX_BATCH [REPS]]]");
   const std::filesystem::path dir = argv[2];
   const herdsman_gpu::SchemaParams sp = parse_params(0, argv[3]);
   const int parts = std::atoi(argv[4]), rows = std::atoi(argv[5]);
@@ -108,6 +110,7 @@ static int bench(int argc, char **argv) {
   cfg.schemas = {sp};
   if (argc > 6) cfg.lanes_per_device = (uint32_t)std::atoi(argv[6]);
   if (argc > 7) cfg.max_batch = (uint32_t)std::atoi(argv[7]);
+  const int reps = argc > 8 ? std::max(1, std::atoi(argv[8])) : 5;
   if (const char *d = std::getenv("WG_DEVICE")) cfg.devices = {std::atoi(d)};
   // ---- synthetic inputs, made on the device with the backend's uniform fill
   fhe_params p = sp.params;
@@ -177,9 +180,10 @@ static int bench(int argc, char **argv) {
     t.circuit = circ;
     return herd::common::task_t{t};
   };
-  double best = 0;
+  std::vector<double> rates;
   GpuWorkerGroup g(cfg);  // one long-lived group, as in a server
-  for (int rep = 0; rep < 3; ++rep) {  // rep 0 warms contexts, keys, pinned and device buffers
+  for (int rep = 0; rep <= reps; ++rep) {  // rep 0 warms contexts, keys, pinned and device buffers
+    if (rep == 1) g.reset_stage_stats();
     std::mutex m;
     std::condition_variable cv;
     int done = 0, errors = 0, next = 0, inflight = 0;
@@ -207,9 +211,25 @@ static int bench(int argc, char **argv) {
     const double rate = (double)parts * rows / dt;
     std::printf("bench rep %d: %d MapTasks x %d rows in %.3f s = %.1f ct-mult+relin/s (%zu workers)\n", rep, parts,
                 rows, dt, rate, g.concurrent_workers());
-    if (rep) best = std::max(best, rate);
+    if (rep) rates.push_back(rate);
   }
-  std::printf("bench: %.1f ct-mult+relin/s (warm group)\n", best);
+  double mean = 0;
+  for (double r : rates) mean += r / rates.size();
+  const auto mm = std::minmax_element(rates.begin(), rates.end());
+  std::printf("bench: %.1f ct-mult+relin/s mean of %zu warm reps (min %.1f, max %.1f); %d partitions x %d rows, "
+              "max_batch %u, %zu lanes\n",
+              mean, rates.size(), *mm.first, *mm.second, parts, rows, cfg.max_batch, g.concurrent_workers());
+  const herdsman_gpu::StageStats st = g.stage_stats();
+  const double lane_s = st.read_s + st.enqueue_s + st.wait_s + st.write_s;
+  std::printf("stages (summed over lanes, warm reps): %llu batches, %llu rows\n", (unsigned long long)st.batches,
+              (unsigned long long)st.rows);
+  const std::pair<const char *, double> rowsv[] = {{"read rows -> pinned (pread)", st.read_s},
+                                                   {"enqueue H2D + kernels + D2H", st.enqueue_s},
+                                                   {"wait for the batch's GPU work", st.wait_s},
+                                                   {"write output rows", st.write_s}};
+  for (const auto &r : rowsv)
+    std::printf("  %-32s %8.3f s  %5.1f%%  %8.2f ms/batch\n", r.first, r.second, 100 * r.second / lane_s,
+                st.batches ? 1e3 * r.second / st.batches : 0.0);
   return 0;
 }
 

@@ -98,6 +98,13 @@ int fhe_memcpy_d2h_async(fhe_ctx *ctx, void *dst, const void *src, size_t bytes)
  * context) for callers without a stream of their own: several contexts on one
  * device then run concurrently, e.g. the worker group's lanes */
 int fhe_use_own_stream(fhe_ctx *ctx);
+/* stream marks for pipelined callers: fhe_mark records the work enqueued so far
+ * on the context's stream in `slot` (< FHE_MAX_MARKS, re-recording overwrites);
+ * fhe_wait_mark blocks the calling thread until that work is done, so a worker
+ * can recycle the staging buffers of batch k while batch k+1 runs */
+#define FHE_MAX_MARKS 16u
+int fhe_mark(fhe_ctx *ctx, uint32_t slot);
+int fhe_wait_mark(fhe_ctx *ctx, uint32_t slot);
 
 /* ---- RNS primitives: data [n_polys][n_limbs][N]; limb l uses modulus mod_begin+l */
 int fhe_ntt_fwd(fhe_ctx *ctx, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs);

@@ -167,6 +167,35 @@ def test_bench_launcher_spawns_ranks_dry_run():
     assert line["elapsed"] >= 0.02  # the slower rank's time
 
 
+def test_bench_driver_argv_eight_ranks_dry_run():
+    """The driver's exact 8-GPU launch (torch.distributed.run, --nproc-per-node 8,
+    127.0.0.1) with --dry-run appended: 8 ranks, shards of 1024 by herdsman's
+    partition rule, n_gpus and the per-rank list cover all 8."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "8", "--steps", "5", "--warmup", "2", "--dry-run"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["ranks"] == 8 and line["n_gpus"] == 8
+    assert sorted(sh[1] for sh in line["shards"]) == [1024] * 8
+    assert all(sh[1] == sh[2] for sh in line["shards"])  # each rank's wave plan covers its shard once
+    assert len(line["per_rank_ct_mult_per_s"]) == 8 and line["steps"] == 5 and line["warmup"] == 2
+    assert len({sh[3] for sh in line["shards"]}) == 8  # eight processes
+
+
 def test_wave_plan_covers_each_shard_once():
     import importlib.util
 

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Stall diagnosis of the roofline kernel pair (forward NTT column + row pass)
+# on the GPU box: wave-state counters (issue stall vs parked vs active), LDS
+# and memory instruction counts, L2 hit rate.  One counter group per run.
+# Usage: tools/diag_stall.sh OUTDIR
+set -e
+OUT=${1:-gpurun_out/stall}
+export TMPDIR=/tmp
+mkdir -p "$OUT"
+R="python3 bench.py --roofline-only --no-cpu --ntt-reps 10"
+timeout -s KILL 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+i=0
+for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES SQ_BUSY_CYCLES" \
+           "TCC_HIT_sum TCC_MISS_sum" \
+           "TA_BUSY_avr TA_TA_BUSY_sum" \
+           "TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d "$OUT/p$i" -o run -- $R > "$OUT/p$i.log" 2>&1
+done
+echo stall passes done
