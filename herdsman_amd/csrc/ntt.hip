@@ -389,6 +389,23 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
       }
     }
     if constexpr (!COLS && G != 0) {
+      // EPI_KSQ: the key-switching operands (ext and key words, KD of each per
+      // element) are software-pipelined PD elements deep, and the first PD
+      // elements' loads are in flight across the re-layout barrier
+      constexpr int KD = is_ksq(EPI) ? ksq_digits(EPI) : 1;
+      constexpr int PD = is_ksq(EPI) && SP ? 2 : 1;
+      u64 ek[PD + 1][2 * KD];
+      if constexpr (is_ksq(EPI)) {
+#pragma unroll
+        for (int r = 0; r < PD; ++r) {
+          const u32 kr = Grp<S, LOGR, 0>::k_reg(r);
+#pragma unroll
+          for (int j = 0; j < KD; ++j) {
+            ek[r][j] = ld_b(ep.kext + j * ep.ext_j + kr, voff);
+            ek[r][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
+          }
+        }
+      }
       // row pass ending in a group whose lanes each own contiguous words:
       // re-layout through LDS so the HBM store is coalesced (group-0 layout)
       const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
@@ -413,12 +430,19 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
             // position: acc_Q never makes an HBM round trip.  Each product is
             // below 1.5q (2q generic), so one subtraction of 4q (WIDE) leaves
             // the lazy sum below 4q; otherwise it is made canonical.
-            constexpr int KD = ksq_digits(EPI);
+            if (r + PD < R) {
+              const u32 kn = G0::k_reg(r + PD);
+#pragma unroll
+              for (int j = 0; j < KD; ++j) {
+                ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + j * ep.ext_j + kn, voff);
+                ek[(r + PD) % (PD + 1)][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
+              }
+            }
             u64 e[KD], k[KD], pr[KD];
 #pragma unroll
             for (int j = 0; j < KD; ++j) {
-              e[j] = ld_b(ep.kext + j * ep.ext_j + kr, voff);
-              k[j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
+              e[j] = ek[r % (PD + 1)][j];
+              k[j] = ek[r % (PD + 1)][KD + j];
             }
             if constexpr (SP) {
               mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
@@ -476,12 +500,30 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
     using GZ = Grp<S, LOGR, 0>;
     voff = (gb + GZ::k_thr(ts)) << 3;
     if constexpr (EPI == PRO_TENSOR) {
-      // the CKKS tensor formulas, element-wise at the coalesced positions
+      // the CKKS tensor formulas, element-wise at the coalesced positions.
+      // Software-pipelined PD elements deep: the operand loads of element
+      // r + PD are issued before element r's stores (the outputs may alias the
+      // operands element-wise only, so the compiler would otherwise wait for
+      // each element's loads right after the previous element's stores)
+      constexpr int PD = SP ? 2 : 0;  // the generic products need the registers
+      u64 op[PD + 1][4];
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        const u32 kr = GZ::k_reg(r);
+        op[r][0] = ld_b(ep.a0 + kr, voff), op[r][1] = ld_b(ep.a1 + kr, voff);
+        op[r][2] = ld_b(ep.b0 + kr, voff), op[r][3] = ld_b(ep.b1 + kr, voff);
+      }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const u32 kr = GZ::k_reg(r);
-        const u64 a0 = ld_b(ep.a0 + kr, voff), a1 = ld_b(ep.a1 + kr, voff);
-        const u64 b0 = ld_b(ep.b0 + kr, voff), b1 = ld_b(ep.b1 + kr, voff);
+        if (r + PD < R) {
+          const u32 kn = GZ::k_reg(r + PD);
+          u64(&o)[4] = op[(r + PD) % (PD + 1)];
+          o[0] = ld_b(ep.a0 + kn, voff), o[1] = ld_b(ep.a1 + kn, voff);
+          o[2] = ld_b(ep.b0 + kn, voff), o[3] = ld_b(ep.b1 + kn, voff);
+        }
+        const u64 a0 = op[r % (PD + 1)][0], a1 = op[r % (PD + 1)][1];
+        const u64 b0 = op[r % (PD + 1)][2], b1 = op[r % (PD + 1)][3];
         st_b(ep.o0 + kr, voff, mul_mod<SP>(a0, b0, mi));
         U128 s = mul128(a0, b1);
         mac128(s, a1, b0);

@@ -109,10 +109,16 @@ class PartitionWriter {
   PartitionWriter &operator=(const PartitionWriter &) = delete;
   // one row = `parts` byte ranges, written as u32 length + the ranges
   void append(const std::vector<std::pair<const void *, size_t>> &parts);
+  // rows written in parallel: claim() reserves `bytes` at the end of the file
+  // (one thread), write_row_at() writes one row (u32 length + parts) at a
+  // claimed offset; calls on disjoint ranges may run concurrently
+  uint64_t claim(uint64_t bytes);
+  void write_row_at(uint64_t off, const std::vector<std::pair<const void *, size_t>> &parts) const;
   void commit();
 
  private:
   std::filesystem::path path_, tmp_;
+  uint64_t end_ = 0;
   int fd_ = -1;
   bool done_ = false, durable_ = false;
 };

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <exception>
 #include <stdexcept>
 #include <string>
 
@@ -155,7 +156,7 @@ PartitionWriter::~PartitionWriter() {
   if (!done_) ::unlink(tmp_.c_str());
 }
 
-void PartitionWriter::append(const std::vector<std::pair<const void *, size_t>> &parts) {
+void PartitionWriter::write_row_at(uint64_t off, const std::vector<std::pair<const void *, size_t>> &parts) const {
   uint32_t len = 0;
   for (const auto &pr : parts) len += (uint32_t)pr.second;
   std::vector<iovec> iov;
@@ -163,12 +164,13 @@ void PartitionWriter::append(const std::vector<std::pair<const void *, size_t>> 
   for (const auto &pr : parts) iov.push_back(iovec{const_cast<void *>(pr.first), pr.second});
   size_t todo = 4 + (size_t)len, first = 0;
   while (todo) {
-    const ssize_t w = ::writev(fd_, iov.data() + first, (int)(iov.size() - first));
+    const ssize_t w = ::pwritev(fd_, iov.data() + first, (int)(iov.size() - first), (off_t)off);
     if (w < 0) {
       if (errno == EINTR) continue;
       throw std::runtime_error("write failed " + tmp_.string());
     }
     todo -= (size_t)w;
+    off += (uint64_t)w;
     size_t adv = (size_t)w;
     while (adv && first < iov.size()) {  // partial write: skip what went out
       if (adv >= iov[first].iov_len) {
@@ -181,6 +183,18 @@ void PartitionWriter::append(const std::vector<std::pair<const void *, size_t>> 
       }
     }
   }
+}
+
+uint64_t PartitionWriter::claim(uint64_t bytes) {
+  const uint64_t at = end_;
+  end_ += bytes;
+  return at;
+}
+
+void PartitionWriter::append(const std::vector<std::pair<const void *, size_t>> &parts) {
+  uint64_t len = 4;
+  for (const auto &pr : parts) len += pr.second;
+  write_row_at(claim(len), parts);
 }
 
 void PartitionWriter::commit() {
@@ -203,6 +217,31 @@ void PartitionWriter::commit() {
 
 // ------------------------------------------------------------- device state
 namespace {
+
+// f(i) for i in [0, n) on up to `threads` threads (contiguous chunks); the
+// first exception is rethrown after every thread has joined
+template <class F>
+void parallel_for(size_t n, unsigned threads, F f) {
+  threads = (unsigned)std::max<size_t>(1, std::min<size_t>(threads, n));
+  if (threads == 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::exception_ptr err;
+  std::mutex em;
+  std::vector<std::thread> pool;
+  for (unsigned t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      try {
+        for (size_t i = n * t / threads; i < n * (t + 1) / threads; ++i) f(i);
+      } catch (...) {
+        std::lock_guard lk(em);
+        if (!err) err = std::current_exception();
+      }
+    });
+  for (auto &th : pool) th.join();
+  if (err) std::rethrow_exception(err);
+}
 
 void ck(fhe_ctx *c, int rc, const char *what) {
   if (rc != FHE_OK) throw std::runtime_error(std::string(what) + ": " + fhe_last_error(c));
@@ -629,7 +668,7 @@ const DevBuf &galois_key(const SchemaCtx &s, const KeySet &ks, int32_t steps, ui
 // H2D, the program's ops and D2H on the lane's stream and mark the slot.
 // Nothing waits for the GPU here.
 void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vector<Instr> &prog,
-                       const PartitionIndex &rows, size_t r0, size_t n, StageStats &st) {
+                       const PartitionIndex &rows, size_t r0, size_t n, unsigned io_threads, StageStats &st) {
   const SchemaCtx &s = ls.s;
   Slot &sl = ls.slot[si];
   sl.r0 = r0;
@@ -645,12 +684,12 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
         if (sl.in.size() <= push) sl.in.push_back(std::make_unique<Pinned>());
         uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[push++]->reserve(s.ctx, cw * n * 8));
         const auto t_r = std::chrono::steady_clock::now();
-        for (size_t r = 0; r < n; ++r) {
+        parallel_for(n, io_threads, [&](size_t r) {
           CtHeader h;
           rows.read(r0 + r, (size_t)ins.arg * one, &h, sizeof(h));
           check_ct_header(s, h);
           rows.read(r0 + r, (size_t)ins.arg * one + sizeof(h), host + r * cw, cw * 8);
-        }
+        });
         read_s += secs_since(t_r);
         ArenaBuf d(*ls.arena, cw * n);
         ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, d.p, host, cw * n * 8), "h2d");
@@ -700,7 +739,7 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
 
 // Second half: wait for the slot's mark (its D2H has landed, its H2D sources
 // are free again) and append the batch's rows to the output partition.
-void finish_map_batch(LaneSchema &ls, int si, PartitionWriter &out, StageStats &st) {
+void finish_map_batch(LaneSchema &ls, int si, PartitionWriter &out, unsigned io_threads, StageStats &st) {
   const SchemaCtx &s = ls.s;
   Slot &sl = ls.slot[si];
   auto t0 = std::chrono::steady_clock::now();
@@ -710,7 +749,10 @@ void finish_map_batch(LaneSchema &ls, int si, PartitionWriter &out, StageStats &
   const size_t cw = s.ct_words();
   const uint64_t *host = reinterpret_cast<const uint64_t *>(sl.out.p);
   const CtHeader h = ct_header(s);
-  for (size_t r = 0; r < sl.n; ++r) out.append({{&h, sizeof(h)}, {host + r * cw, cw * 8}});
+  const uint64_t row_bytes = 4 + sizeof(h) + cw * 8;
+  const uint64_t base = out.claim(row_bytes * sl.n);
+  parallel_for(sl.n, io_threads,
+               [&](size_t r) { out.write_row_at(base + r * row_bytes, {{&h, sizeof(h)}, {host + r * cw, cw * 8}}); });
   st.write_s += secs_since(t0);
   st.batches += 1;
   st.rows += sl.n;
@@ -756,11 +798,11 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         for (size_t r0 = 0; r0 < rows.size(); r0 += config_.max_batch, ++k) {
           const size_t n = std::min<size_t>(config_.max_batch, rows.size() - r0);
           const int si = (int)(k & 1);
-          enqueue_map_batch(ls, si, *ks, prog, rows, r0, n, stats);
-          if (pending >= 0) finish_map_batch(ls, pending, out, stats);
+          enqueue_map_batch(ls, si, *ks, prog, rows, r0, n, config_.io_threads, stats);
+          if (pending >= 0) finish_map_batch(ls, pending, out, config_.io_threads, stats);
           pending = si;
         }
-        if (pending >= 0) finish_map_batch(ls, pending, out, stats);
+        if (pending >= 0) finish_map_batch(ls, pending, out, config_.io_threads, stats);
         out.commit();
       } else {
         // ReduceTask: combine every row of every input partition into one

@@ -87,6 +87,7 @@ struct GpuWorkerGroupConfig {
   uint32_t lanes_per_device = 4;      // concurrent tasks per device (context + stream each)
   uint32_t max_batch = 64;            // rows per batched GPU call
   bool durable_outputs = false;       // fsync output partitions (PartitionWriter)
+  uint32_t io_threads = 4;            // threads per lane reading / writing a batch's rows
 };
 
 class GpuWorkerGroup : public IWorkerGroup {
