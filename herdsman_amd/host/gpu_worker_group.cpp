@@ -780,6 +780,7 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
     Status st = Status::COMPLETED;
     LaneSchema *cur = nullptr;
     StageStats stats;
+    const auto t_task = std::chrono::steady_clock::now();
     try {
       if (std::holds_alternative<herd::common::MapTask>(job.task)) {
         const auto &t = std::get<herd::common::MapTask>(job.task);
@@ -856,6 +857,8 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
       // buffers: let them finish before the next task reuses (or regrows) them
       if (cur) (void)fhe_synchronize(cur->s.ctx);
     }
+    stats.task_s = secs_since(t_task);
+    stats.tasks = 1;
     {
       std::lock_guard lk(stats_m_);
       stats_ += stats;

@@ -67,8 +67,11 @@ inline std::vector<SchemaParams> default_schemas() {
 // writing output rows.
 struct StageStats {
   double read_s = 0, enqueue_s = 0, wait_s = 0, write_s = 0;
-  uint64_t batches = 0, rows = 0;
+  double task_s = 0;  // whole tasks on the lanes, open to commit
+  uint64_t batches = 0, rows = 0, tasks = 0;
   StageStats &operator+=(const StageStats &o) {
+    task_s += o.task_s;
+    tasks += o.tasks;
     read_s += o.read_s;
     enqueue_s += o.enqueue_s;
     wait_s += o.wait_s;

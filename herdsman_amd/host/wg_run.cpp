@@ -111,6 +111,7 @@ static int bench(int argc, char **argv) {
   if (argc > 6) cfg.lanes_per_device = (uint32_t)std::atoi(argv[6]);
   if (argc > 7) cfg.max_batch = (uint32_t)std::atoi(argv[7]);
   const int reps = argc > 8 ? std::max(1, std::atoi(argv[8])) : 5;
+  if (const char *t = std::getenv("WG_IO_THREADS")) cfg.io_threads = (uint32_t)std::max(1, std::atoi(t));
   if (const char *d = std::getenv("WG_DEVICE")) cfg.devices = {std::atoi(d)};
   // ---- synthetic inputs, made on the device with the backend's uniform fill
   fhe_params p = sp.params;
@@ -170,12 +171,13 @@ static int bench(int argc, char **argv) {
   herd::common::Circuit circ;
   circ.program = {{herd::common::CtOp::PUSH_INPUT, 0}, {herd::common::CtOp::PUSH_INPUT, 1},
                   {herd::common::CtOp::MUL_RELIN, 0}};
+  int rep_no = 0;  // each repetition writes a fresh output frame, as every herdsman job does
   auto make = [&](int part) {
     herd::common::MapTask t;
     t.session_uuid = {"bench"};
     t.input_data_frame_ptr.pointer = {{"in"}, (uint32_t)part};
     t.input_data_frame_ptr.row_count = (uint64_t)rows;
-    t.output_data_frame_ptr = {{"out"}, (uint32_t)part};
+    t.output_data_frame_ptr = {{"out" + std::to_string(rep_no)}, (uint32_t)part};
     t.crypto_key_ptr.schema_type = herd::common::SchemaType::CKKS;
     t.circuit = circ;
     return herd::common::task_t{t};
@@ -184,6 +186,8 @@ static int bench(int argc, char **argv) {
   GpuWorkerGroup g(cfg);  // one long-lived group, as in a server
   for (int rep = 0; rep <= reps; ++rep) {  // rep 0 warms contexts, keys, pinned and device buffers
     if (rep == 1) g.reset_stage_stats();
+    rep_no = rep;
+    if (rep > 0) std::filesystem::remove_all(cfg.storage_dir / "bench" / ("out" + std::to_string(rep - 1)));
     std::mutex m;
     std::condition_variable cv;
     int done = 0, errors = 0, next = 0, inflight = 0;
@@ -217,12 +221,15 @@ static int bench(int argc, char **argv) {
   for (double r : rates) mean += r / rates.size();
   const auto mm = std::minmax_element(rates.begin(), rates.end());
   std::printf("bench: %.1f ct-mult+relin/s mean of %zu warm reps (min %.1f, max %.1f); %d partitions x %d rows, "
-              "max_batch %u, %zu lanes\n",
-              mean, rates.size(), *mm.first, *mm.second, parts, rows, cfg.max_batch, g.concurrent_workers());
+              "max_batch %u, %zu lanes, %u io threads per lane\n",
+              mean, rates.size(), *mm.first, *mm.second, parts, rows, cfg.max_batch, g.concurrent_workers(),
+              cfg.io_threads);
   const herdsman_gpu::StageStats st = g.stage_stats();
   const double lane_s = st.read_s + st.enqueue_s + st.wait_s + st.write_s;
-  std::printf("stages (summed over lanes, warm reps): %llu batches, %llu rows\n", (unsigned long long)st.batches,
-              (unsigned long long)st.rows);
+  std::printf("stages (summed over lanes, warm reps): %llu tasks, %llu batches, %llu rows; task time %.3f s "
+              "(%.1f ms per task, of which the stages below %.1f ms)\n",
+              (unsigned long long)st.tasks, (unsigned long long)st.batches, (unsigned long long)st.rows, st.task_s,
+              st.tasks ? 1e3 * st.task_s / st.tasks : 0.0, st.tasks ? 1e3 * lane_s / st.tasks : 0.0);
   const std::pair<const char *, double> rowsv[] = {{"read rows -> pinned (pread)", st.read_s},
                                                    {"enqueue H2D + kernels + D2H", st.enqueue_s},
                                                    {"wait for the batch's GPU work", st.wait_s},
