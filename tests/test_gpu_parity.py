@@ -189,11 +189,13 @@ def test_ckks_rotate_c4(hb):
 
 
 @pytest.mark.parametrize("log_n,L,K,dnum", [(13, 7, 3, 3), (15, 8, 2, 4), (15, 5, 1, 5), (12, 12, 2, 12),
-                                            (12, 18, 2, 18)])
+                                            (12, 18, 2, 18), (15, 10, 4, 2), (15, 4, 2, 1)])
 def test_keyswitch_vs_oracle(hb, log_n, L, K, dnum):
     """(13,7,3,3): ragged digits (alpha=3, last digit 1 limb); (15,8,2,4): 4 digits;
     (15,5,1,5): 5 single-limb digits; 12 and 18 digits: the register-cached (<= 16) and
-    streamed (> 16) key paths of the inner product."""
+    streamed (> 16) key paths of the inner product; (15,10,4,2): alpha 5, so the fused
+    ModDown (and its fused Q-limb inner product) runs after the separate ModUp kernel;
+    (15,4,2,1): one digit (the inner product fused into the finish with one term)."""
     o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum)
     d = o.uniform((2, L, 1 << log_n), seed=30)
     k = o.uniform(o.key_shape(), seed=31)

@@ -22,10 +22,12 @@ def short(name):
 def main(d, steps):
     f = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "true, false, true, 2>" in r["Kernel_Name"]]
+    # a step starts at the tensor-prologue INTT row pass (EPI 2) and ends at its
+    # ModDown-finish row pass (EPI 1, or 6..9 with the fused inner product);
+    # round-3 kernels carry a trailing lazy-schedule parameter
+    starts = [i for i, r in enumerate(rows) if re.search(r"true, false, true, 2(, \d)?>", r["Kernel_Name"])]
     first = starts[-steps]
-    # a step ends at its fused-combine row pass (EPI 1)
-    last = max(i for i, r in enumerate(rows) if "false, false, true, 1>" in r["Kernel_Name"])
+    last = max(i for i, r in enumerate(rows) if re.search(r"false, false, true, [16789](, \d)?>", r["Kernel_Name"]))
     agg = defaultdict(lambda: [0, 0.0, 0, 0])
     for r in rows[first:last + 1]:
         k = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]))
