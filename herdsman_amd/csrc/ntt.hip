@@ -33,6 +33,10 @@
 
 #include "context.hpp"
 
+#ifndef MODUP_COL_SPLIT
+#define MODUP_COL_SPLIT 1
+#endif
+
 namespace {
 
 struct NttArgs {
@@ -101,7 +105,10 @@ struct NttArgs {
 // that produces its input
 // EPI_KSQ + d - 1: EPI_COMBINE with the Q limbs' key-switching inner product
 // over d = 1..4 digits fused in (the digit count is compile-time)
-enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, PRO_CONV = 5, EPI_KSQ = 6 };
+// PRO_CONV + ns - 1: the conversion prologue over ns = 1..4 source limbs (compile-time)
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, EPI_KSQ = 6, PRO_CONV = 11 };
+__host__ __device__ constexpr bool is_conv(int e) { return e >= PRO_CONV && e < PRO_CONV + 4; }
+__host__ __device__ constexpr int conv_ns(int e) { return e - PRO_CONV + 1; }
 __host__ __device__ constexpr bool is_ksq(int e) { return e >= EPI_KSQ && e < EPI_KSQ + 4; }
 __host__ __device__ constexpr int ksq_digits(int e) { return e - EPI_KSQ + 1; }
 __host__ __device__ constexpr bool is_combine(int e) { return e == EPI_COMBINE || is_ksq(e); }
@@ -121,7 +128,6 @@ struct EpiRow {
   u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is
   const u64 *src;  // PRO_CONV: source limb 0 of this poly (limb i at src + i N)
   u64 h[4];        // PRO_CONV: h[i][m] of this workgroup's target limb
-  u32 ns;
 };
 
 // LDS slot of element k of sub-transform w: one pad word per 16 words and per
@@ -584,20 +590,22 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
   } else {
     using GF = Grp<S, LOGR, G0>;
     voff = (gb + (GF::k_thr(ts) << PG::LS)) << 3;
-    if constexpr (EPI == PRO_CONV) {
-      // the base conversion (conv_apply, oracle) of this element from the ns
-      // source limbs at the same position, 4 elements at a time
+    if constexpr (is_conv(EPI)) {
+      // the base conversion (conv_apply, oracle) of this element from the NS
+      // source limbs at the same position, 4 elements at a time (NS is a
+      // template parameter: no per-term predication)
+      constexpr int NS = conv_ns(EPI);
       constexpr size_t NW = (size_t)1 << LOG_N;
 #pragma unroll
       for (int c0 = 0; c0 < R; c0 += 4) {
-        u64 sv[4][4];
+        u64 sv[4][NS];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            sv[j][i] = i < (int)ep.ns ? ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff) : 0;
+          for (int i = 0; i < NS; ++i)
+            sv[j][i] = ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont_lazy<4, SP>(sv[j], ep.h, 1, ep.ns, mi);  // < 4q
+        for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont_lazy<NS, SP>(sv[j], ep.h, 1, NS, mi);  // < 4q
       }
     } else {
       // the first forward pass may read out of place (NttArgs::src)
@@ -630,9 +638,9 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int WM>
 __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NTT_MINW : 1) ntt_pass(NttArgs a) {
   static_assert(is_combine(EPI) || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
-                    EPI == PRO_BFVT || EPI == PRO_CONV,
+                    EPI == PRO_BFVT || is_conv(EPI),
                 "ntt_pass epilogues");
-  static_assert(EPI != PRO_CONV || (!INV && COLS), "the conversion prologue feeds a forward column pass");
+  static_assert(!is_conv(EPI) || (!INV && COLS), "the conversion prologue feeds a forward column pass");
   static_assert(!is_combine(EPI) || (!INV && !COLS), "epilogues follow a forward row pass");
   static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT) || (INV && !COLS),
                 "prologues feed an inverse row pass");
@@ -673,7 +681,7 @@ __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NT
     bx = g % gridDim.x;
     act = g / gridDim.x;
   }
-  if constexpr (EPI == PRO_CONV) {
+  if constexpr (is_conv(EPI)) {
     // the T target limbs of one source block (poly, column block) run on
     // consecutive workgroup ids of ONE XCD (ids are dealt round-robin over the
     // 8 XCDs), so the ns source limbs come from that XCD's L2 after the first
@@ -753,11 +761,10 @@ __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NT
     ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
     ep.g = a.t_g;
   }
-  if constexpr (EPI == PRO_CONV) {
+  if constexpr (is_conv(EPI)) {
     ep.src = a.c_src + (((size_t)poly * a.c_src_stride + a.c_src_first) << LOG_N);
-    ep.ns = a.c_ns;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ep.h[i] = i < (int)a.c_ns ? a.c_h[(size_t)i * a.c_nd + act] : 0;
+    for (int i = 0; i < conv_ns(EPI); ++i) ep.h[i] = a.c_h[(size_t)i * a.c_nd + act];
   }
   if constexpr (!INV && WM == 2) {
     // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)
@@ -806,7 +813,7 @@ int launch_fwd(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
 
 template <int LOG_N, int S, int W, bool COLS, int EPI = EPI_NONE>
 int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
-  if constexpr (is_combine(EPI) || EPI == PRO_CONV) {
+  if constexpr (is_combine(EPI) || is_conv(EPI)) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
     return c->special ? launch_fwd<LOG_N, S, W, COLS, EPI, true>(c, a, n_jobs)
                       : launch_fwd<LOG_N, S, W, COLS, EPI, false>(c, a, n_jobs);
@@ -860,6 +867,17 @@ int row_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
     case 17: return launch_pass<17, 9, 8, false, EPI>(c, a, inv, n_jobs);
   }
   return fhe_fail(c, FHE_ERR_UNSUPPORTED, "row_pass: log_n");
+}
+
+// the forward column pass with the conversion prologue over a.c_ns sources
+int conv_col_pass(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
+  switch (a.c_ns) {
+    case 1: return col_pass<PRO_CONV>(c, a, false, n_jobs);
+    case 2: return col_pass<PRO_CONV + 1>(c, a, false, n_jobs);
+    case 3: return col_pass<PRO_CONV + 2>(c, a, false, n_jobs);
+    case 4: return col_pass<PRO_CONV + 3>(c, a, false, n_jobs);
+  }
+  return fhe_fail(c, FHE_ERR_UNSUPPORTED, "conversion prologue: 1..4 source limbs");
 }
 
 }  // namespace
@@ -955,7 +973,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
         a.c_ns = pro->ns;
         a.c_nd = pro->nd;
         a.c_h = pro->h;
-        rc = col_pass<PRO_CONV>(c, a, false, n_jobs);
+        rc = conv_col_pass(c, a, n_jobs);
       } else {
         rc = col_pass(c, a, false, n_jobs);
       }
@@ -1001,18 +1019,27 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
     a.c_nd = tab.nd;
     a.c_h = tab.h;
     const u32 n_jobs = np * a.map.cnt;
-    int rc = col_pass<PRO_CONV>(c, a, false, n_jobs);
-    if (rc) return rc;
-    // the row pass as one launch per modulus class where that splits the
-    // targets into a Q part and a P part of one class each (ntt_pass WM)
+    // one launch per modulus class where that splits the targets into a Q part
+    // and a P part of one class each (ntt_pass WM: a kernel carrying both lazy
+    // schedules needs 150-160 VGPRs, 3 waves per SIMD); the P part's targets
+    // start at column L - alpha of the conversion table
     NttArgs aq = a, ap = a;
     aq.map = LimbMap{a.map.base, a.map.poly_stride, L - (hi - lo), 0, lo, hi - lo, 0, np};
     ap.map = LimbMap{a.map.base, a.map.poly_stride, c->K, L, c->K, 0, 0, np};
+    ap.c_h = tab.h + (L - (hi - lo));
     const int wq = wide_mode(c, aq.map), wp = wide_mode(c, ap.map);
+    int rc;
     if (wq != 2 && wp != 2 && wq != wp && aq.map.cnt && ap.map.cnt) {
+#if MODUP_COL_SPLIT
+      if ((rc = conv_col_pass(c, aq, np * aq.map.cnt))) return rc;
+      if ((rc = conv_col_pass(c, ap, np * ap.map.cnt))) return rc;
+#else
+      if ((rc = conv_col_pass(c, a, n_jobs))) return rc;
+#endif
       if ((rc = row_pass(c, aq, false, np * aq.map.cnt))) return rc;
       rc = row_pass(c, ap, false, np * ap.map.cnt);
     } else {
+      if ((rc = conv_col_pass(c, a, n_jobs))) return rc;
       rc = row_pass(c, a, false, n_jobs);
     }
     if (rc) return rc;
