@@ -10,10 +10,11 @@
 //         family, still NTT-friendly for every N <= 2^31): q' = -q^-1 = -1 mod
 //         2^32, so each of the two 32-bit Montgomery rounds needs ONE
 //         v_mad_u64_u32 (m * q_hi) -- 2 multiplies in total;
-//       - generic odd moduli (explicit OpenFHE-style primes): one 64-bit round
-//         with q' = -q^-1 mod 2^64, 7 multiplies (mont_reduce, used after the
-//         128-bit sums of the dot products); a single product uses two 32-bit
-//         CIOS rounds instead (mont_mul_gen: 8 + 2 multiplies in all);
+//       - generic odd moduli (explicit OpenFHE-style primes): two 32-bit
+//         rounds with q' = -q^-1 mod 2^32, 4 v_mad_u64_u32 + 2 v_mul_lo_u32
+//         (mont_reduce, used after the 128-bit sums of the dot products; the
+//         host keeps one 64-bit round); a single product interleaves the same
+//         rounds with the operand words (mont_mul_gen: 8 + 2 multiplies);
 //   * every constant operand (twiddles, CRT constants, N^-1, P^-1) is stored
 //     pre-multiplied by R, so mont_mul(x, cR) = x * c exactly: a twiddle
 //     multiply costs 4 + 2 = 6 multiplies (Shoup needs 10);
@@ -29,6 +30,10 @@ typedef uint64_t u64;
 typedef uint32_t u32;
 
 #define HD __host__ __device__ __forceinline__
+
+#ifndef GEN_RED_CIOS
+#define GEN_RED_CIOS 1  // generic mont_reduce on the device: two 32-bit rounds (0: one 64-bit round)
+#endif
 
 struct ModInfo {
   u64 q;
@@ -87,8 +92,28 @@ HD u64 mont_reduce(U128 T, const ModInfo &m) {
     const u64 M2 = (u64)(0u - t1) * m.q_hi + (t1 != 0);
     return (((u64)top << 32) | (r >> 32)) + M2;
   } else {
+#if defined(__HIP_DEVICE_COMPILE__) && GEN_RED_CIOS
+    // two 32-bit Montgomery rounds, quotient digit m_k = t_k q' mod 2^32:
+    // 2 v_mul_lo_u32 + 4 v_mad_u64_u32 (the 64-bit round: 3 for the quotient
+    // + 4 for its high product).  T1 = (T + m0 q) / 2^32 < q (2^32 + 1) is 96
+    // bits wide; T2 = (T1 + m1 q) / 2^32 < 2q.
+    const u32 q0 = (u32)m.q, q1 = (u32)(m.q >> 32), qi = (u32)m.qinv_neg;
+    const u32 t0 = (u32)T.lo;
+    const u32 m0 = t0 * qi;
+    const u64 A = (u64)m0 * q0 + t0;  // low word 0
+    const u64 B = (u64)m0 * q1 + ((T.lo >> 32) + (A >> 32));
+    const u64 sh = T.hi << 32;
+    const u64 L1 = B + sh;
+    const u32 H1 = (u32)(T.hi >> 32) + (L1 < sh);
+    const u32 t1 = (u32)L1;
+    const u32 m1 = t1 * qi;
+    const u64 A2 = (u64)m1 * q0 + t1;
+    const u64 B2 = (u64)m1 * q1 + ((L1 >> 32) + (A2 >> 32));
+    return B2 + ((u64)H1 << 32);
+#else
     const u64 mm = T.lo * m.qinv_neg;
     return T.hi + mulhi64(mm, m.q) + (T.lo != 0);
+#endif
   }
 }
 

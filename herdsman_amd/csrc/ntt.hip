@@ -33,6 +33,12 @@
 
 #include "context.hpp"
 
+#ifndef KSQ_PD
+#define KSQ_PD 2  // EPI_KSQ operand prefetch depth (elements; 3 measured no faster, profiles/r03/ab_ksq_pd_aut.txt)
+#endif
+#ifndef AUT_PD
+#define AUT_PD 2  // PRO_AUTOMORPH gather prefetch depth (elements)
+#endif
 #ifndef MODUP_COL_SPLIT
 #define MODUP_COL_SPLIT 1
 #endif
@@ -399,7 +405,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
       // element) are software-pipelined PD elements deep, and the first PD
       // elements' loads are in flight across the re-layout barrier
       constexpr int KD = is_ksq(EPI) ? ksq_digits(EPI) : 1;
-      constexpr int PD = is_ksq(EPI) && SP ? 2 : 1;
+      constexpr int PD = is_ksq(EPI) && SP ? KSQ_PD : 1;
       u64 ek[PD + 1][2 * KD];
       if constexpr (is_ksq(EPI)) {
 #pragma unroll
@@ -560,14 +566,29 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       // NTT-domain automorphism: slot k holds a(psi^e), e = 2 brv(k) + 1, and
       // sigma_g(a)(psi^e) = a(psi^(e g)).  The 64 lanes of a load read one
       // aligned 64-slot block of the source (g only permutes inside it).
+      // Software-pipelined like PRO_TENSOR: element r + PD's gathers are
+      // issued before element r's stores
       constexpr u32 MASK = (2u << LOG_N) - 1;
+      constexpr int PD = AUT_PD;
+      const auto src_of = [&](int r) {
+        const u32 k = (voff >> 3) + GZ::k_reg(r);
+        const u32 e = (((__brev(k) >> (32 - LOG_N)) << 1) | 1) * ep.g & MASK;
+        return (__brev(e >> 1) >> (32 - LOG_N)) << 3;
+      };
+      u64 y[PD + 1][2];
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        const u32 sr = src_of(r);
+        y[r][0] = ld_b(ep.a0, sr), y[r][1] = ld_b(ep.a1, sr);
+      }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const u32 kr = GZ::k_reg(r);
-        const u32 k = (voff >> 3) + kr;
-        const u32 e = (((__brev(k) >> (32 - LOG_N)) << 1) | 1) * ep.g & MASK;
-        const u32 src = (__brev(e >> 1) >> (32 - LOG_N)) << 3;
-        const u64 y0 = ld_b(ep.a0, src), y1 = ld_b(ep.a1, src);
+        if (r + PD < R) {
+          const u32 sn = src_of(r + PD);
+          y[(r + PD) % (PD + 1)][0] = ld_b(ep.a0, sn), y[(r + PD) % (PD + 1)][1] = ld_b(ep.a1, sn);
+        }
+        const u64 y0 = y[r % (PD + 1)][0], y1 = y[r % (PD + 1)][1];
         st_b(ep.o0 + kr, voff, y0);
         x[r] = y1;
         st_b(ep.ext + kr, voff, csub(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R

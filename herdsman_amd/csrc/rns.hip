@@ -14,6 +14,7 @@
 // (2 multiplies) or the generic one (7 multiplies); see modarith.hpp.
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "context.hpp"
 
@@ -319,20 +320,24 @@ __global__ void __launch_bounds__(EW_BLOCK) automorph_ks_kernel(const u64 *__res
 // Constants for SEAL-style BEHZ (behz_init in the oracle), Montgomery
 // pre-scaled ("_R" = times 2^64 mod the modulus it is used with).
 #define BEHZ_MAXL 24
+// The constant factors that follow a conversion are folded into its weights
+// (a product of canonical residues by c, then by c', is the canonical residue
+// of one product by c c'), so each output costs one Montgomery product fewer
+// than the formula as written (extend: sm_mrq's 2^-32; floor: Q^-1 and the
+// fastbconv_sk weight (B/b_j)^-1, or B^-1 for m_sk).  The outputs are the same
+// residues, bit for bit.
 struct BehzDev {
   u32 L, nB, bsk0;                 // bsk0 = first Bsk modulus id
   u32 neg_inv_q_mod_mt;            // -Q^-1 mod 2^32
   u32 h_mod_mt[BEHZ_MAXL];         // (Q/q_i) mod 2^32
   u64 mt_hinv_R[BEHZ_MAXL];        // 2^32 (Q/q_i)^-1 mod q_i
   u64 t_hinv_R[BEHZ_MAXL];         // t (Q/q_i)^-1 mod q_i
-  u64 h_q_bsk_R[BEHZ_MAXL][BEHZ_MAXL + 1];  // (Q/q_i) mod b_j
-  u64 q_mod_bsk_R[BEHZ_MAXL + 1];  // Q mod b_j
-  u64 inv_mt_bsk_R[BEHZ_MAXL + 1]; // 2^-32 mod b_j
-  u64 inv_q_bsk_R[BEHZ_MAXL + 1];  // Q^-1 mod b_j
-  u64 t_bsk_R[BEHZ_MAXL + 1];      // t mod b_j
-  u64 b_hinv_R[BEHZ_MAXL];         // (B/b_j)^-1 mod b_j
-  u64 h_b_msk_R[BEHZ_MAXL];        // (B/b_j) mod m_sk
-  u64 inv_b_msk_R;                 // B^-1 mod m_sk
+  u64 hx_R[BEHZ_MAXL][BEHZ_MAXL + 1];  // extend: (Q/q_i) 2^-32 mod b_j
+  u64 qx_R[BEHZ_MAXL + 1];             // extend: Q 2^-32 mod b_j
+  u64 hf_R[BEHZ_MAXL][BEHZ_MAXL + 1];  // floor: -(Q/q_i) Q^-1 c_j mod b_j
+  u64 tf_R[BEHZ_MAXL + 1];             // floor: t Q^-1 c_j mod b_j
+                                       //   (c_j = (B/b_j)^-1, for m_sk: B^-1)
+  u64 hbm_R[BEHZ_MAXL];                // floor: (B/b_j) B^-1 mod m_sk
   u64 b_mod_q_R[BEHZ_MAXL];        // B mod q_i
   u64 h_b_q_R[BEHZ_MAXL][BEHZ_MAXL];  // (B/b_j) mod q_i
 };
@@ -367,10 +372,10 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
   u64 *d = xb + ((size_t)((w >> 1) * n_items + item) * 2 + (w & 1)) * nB * N + k;
   for (u32 j = 0; j < nB; ++j) {
     const ModInfo m = mods[bz->bsk0 + j];
-    const u64 xbj = dot_mont<NL, SP>(v, &bz->h_q_bsk_R[0][j], BEHZ_MAXL + 1, L, m);
+    // (sum_i v_i (Q/q_i) + r Q) 2^-32, the 2^-32 folded into the weights
+    const u64 xbj = dot_mont<NL, SP>(v, &bz->hx_R[0][j], BEHZ_MAXL + 1, L, m);
     const u64 rr = r >= 0x80000000u ? (u64)r + m.q - (1ull << 32) : (u64)r;   // centered r mod b
-    const u64 sum = add_mod(xbj, csub(mont_mul<SP>(rr, bz->q_mod_bsk_R[j], m), m.q), m.q);
-    d[j * N] = csub(mont_mul<SP>(sum, bz->inv_mt_bsk_R[j], m), m.q);
+    d[j * N] = add_mod(xbj, csub(mont_mul<SP>(rr, bz->qx_R[j], m), m.q), m.q);
   }
 }
 
@@ -399,25 +404,26 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
       v[i] = csub(mont_mul<SP>(xq[i * N], bz->t_hinv_R[i], m), m.q);  // [t x (Q/q_i)^-1]_{q_i}
     }
   }
-  // fast_floor: ((t x)_b - conv_Q->b(t x)) * Q^-1, then fastbconv_sk weights
+  // fast_floor: ((t x)_b - conv_Q->b(t x)) * Q^-1, then the fastbconv_sk
+  // weight: w_j = (x_b t Q^-1 c_j) + sum_i v_i (-(Q/q_i) Q^-1 c_j), one dot
+  // product and one product (the constants carry Q^-1 and c_j)
   u64 w[NL];
   u64 flsk = 0;
 #pragma unroll
   for (int j = 0; j < NL + 1; ++j) {
     if (j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
-      const u64 cv = dot_mont<NL, SP>(v, &bz->h_q_bsk_R[0][j], BEHZ_MAXL + 1, L, m);
-      const u64 tx = csub(mont_mul<SP>(xb[j * N], bz->t_bsk_R[j], m), m.q);
-      const u64 fl = csub(mont_mul<SP>(sub_mod(tx, cv, m.q), bz->inv_q_bsk_R[j], m), m.q);
-      if (j == (int)nB - 1) flsk = fl;
-      else if (j < NL) w[j] = csub(mont_mul<SP>(fl, bz->b_hinv_R[j], m), m.q);
+      const u64 cv = dot_mont<NL, SP>(v, &bz->hf_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 tx = csub(mont_mul<SP>(xb[j * N], bz->tf_R[j], m), m.q);
+      const u64 wj = add_mod(tx, cv, m.q);
+      if (j == (int)nB - 1) flsk = wj;
+      else if (j < NL) w[j] = wj;
     } else if (j < NL) {
       w[j] = 0;
     }
   }
   const ModInfo msk = mods[bz->bsk0 + nB - 1];
-  const u64 cmsk = dot_mont<NL, SP>(w, bz->h_b_msk_R, 1, nB - 1, msk);
-  const u64 alpha = csub(mont_mul<SP>(sub_mod(cmsk, flsk, msk.q), bz->inv_b_msk_R, msk), msk.q);
+  const u64 alpha = sub_mod(dot_mont<NL, SP>(w, bz->hbm_R, 1, nB - 1, msk), flsk, msk.q);  // B^-1 folded in
   const bool neg = alpha > msk.q / 2;
   const u64 amag = neg ? msk.q - alpha : alpha;
   u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
@@ -711,6 +717,8 @@ int behz_setup(fhe_ctx *c) {
   const u64 *qq = c->moduli.data(), *bsk = c->moduli.data() + bsk0;
   const u64 msk = bsk[nB - 1];
   const u64 mt = 1ull << 32;
+  std::vector<std::vector<u64>> h_q_bsk(L, std::vector<u64>(nB));  // (Q/q_i) mod b_j
+  std::vector<u64> cj(nB);                                          // the floor's c_j
   auto M = host_mulmod;
   auto R = host_to_mont;
   for (u32 i = 0; i < L; ++i) {
@@ -722,11 +730,9 @@ int behz_setup(fhe_ctx *c) {
     // the floor's inputs come from an inverse NTT without its N^-1 (bfv_mul_relin_impl): fold it here
     B->t_hinv_R[i] = R(M(M(hinv, c->t % qq[i], qq[i]), host_inv(c->n % qq[i], qq[i]), qq[i]), qq[i]);
     B->h_mod_mt[i] = (u32)hm;
-    for (u32 j = 0; j < nB; ++j) {
-      u64 p2 = 1;
-      for (u32 k = 0; k < L; ++k) if (k != i) p2 = M(p2, qq[k] % bsk[j], bsk[j]);
-      B->h_q_bsk_R[i][j] = R(p2, bsk[j]);
-    }
+    for (u32 j = 0; j < nB; ++j) h_q_bsk[i][j] = 1;
+    for (u32 j = 0; j < nB; ++j)
+      for (u32 k = 0; k < L; ++k) if (k != i) h_q_bsk[i][j] = M(h_q_bsk[i][j], qq[k] % bsk[j], bsk[j]);
     u64 bm = 1;
     for (u32 k = 0; k + 1 < nB; ++k) bm = M(bm, bsk[k] % qq[i], qq[i]);
     B->b_mod_q_R[i] = R(bm, qq[i]);
@@ -736,30 +742,34 @@ int behz_setup(fhe_ctx *c) {
   u32 inv = (u32)qm;
   for (int it = 0; it < 5; ++it) inv *= 2u - (u32)qm * inv;
   B->neg_inv_q_mod_mt = 0u - inv;
-  for (u32 j = 0; j < nB; ++j) {
-    const u64 b = bsk[j];
-    u64 qmb = 1;
-    for (u32 k = 0; k < L; ++k) qmb = M(qmb, qq[k] % b, b);
-    B->q_mod_bsk_R[j] = R(qmb, b);
-    B->inv_q_bsk_R[j] = R(host_inv(qmb, b), b);
-    B->inv_mt_bsk_R[j] = R(host_inv(mt % b, b), b);
-    B->t_bsk_R[j] = R(M(c->t % b, host_inv(c->n % b, b), b), b);
-  }
+  u64 bmsk = 1;
+  for (u32 k = 0; k + 1 < nB; ++k) bmsk = M(bmsk, bsk[k] % msk, msk);
+  const u64 inv_b_msk = host_inv(bmsk, msk);
   for (u32 j = 0; j + 1 < nB; ++j) {
     u64 bh = 1, bhm = 1;
     for (u32 k = 0; k + 1 < nB; ++k)
       if (k != j) { bh = M(bh, bsk[k] % bsk[j], bsk[j]); bhm = M(bhm, bsk[k] % msk, msk); }
-    B->b_hinv_R[j] = R(host_inv(bh, bsk[j]), bsk[j]);
-    B->h_b_msk_R[j] = R(bhm, msk);
+    cj[j] = host_inv(bh, bsk[j]);
+    B->hbm_R[j] = R(M(bhm, inv_b_msk, msk), msk);
     for (u32 i = 0; i < L; ++i) {
       u64 p2 = 1;
       for (u32 k = 0; k + 1 < nB; ++k) if (k != j) p2 = M(p2, bsk[k] % qq[i], qq[i]);
       B->h_b_q_R[j][i] = R(p2, qq[i]);
     }
   }
-  u64 bmsk = 1;
-  for (u32 k = 0; k + 1 < nB; ++k) bmsk = M(bmsk, bsk[k] % msk, msk);
-  B->inv_b_msk_R = R(host_inv(bmsk, msk), msk);
+  cj[nB - 1] = inv_b_msk;
+  for (u32 j = 0; j < nB; ++j) {
+    const u64 b = bsk[j];
+    u64 qmb = 1;
+    for (u32 k = 0; k < L; ++k) qmb = M(qmb, qq[k] % b, b);
+    const u64 inv_mt = host_inv(mt % b, b), qf = M(host_inv(qmb, b), cj[j], b);  // Q^-1 c_j
+    B->qx_R[j] = R(M(qmb, inv_mt, b), b);
+    B->tf_R[j] = R(M(M(c->t % b, host_inv(c->n % b, b), b), qf, b), b);
+    for (u32 i = 0; i < L; ++i) {
+      B->hx_R[i][j] = R(M(h_q_bsk[i][j], inv_mt, b), b);
+      B->hf_R[i][j] = R((b - M(h_q_bsk[i][j], qf, b)) % b, b);
+    }
+  }
   c->behz = ctx_upload(c, B, sizeof(BehzDev));
   delete B;
   return c->behz ? FHE_OK : FHE_ERR_OOM;

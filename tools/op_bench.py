@@ -1,6 +1,9 @@
 """Time one ciphertext op at a BASELINE config (GPU box), for rocprofv3 runs.
 
-    python tools/op_bench.py bfv_mul|ckks_mul|ckks_rot [--batch 32] [--reps 10]
+    python tools/op_bench.py bfv_mul|ckks_mul|ckks_rot [--batch 32] [--reps 10] [--openfhe-primes]
+
+--openfhe-primes: the CKKS ops on OpenFHE-style primes (q = 1 mod 2N, generic
+Montgomery path) instead of the default q = 1 (mod 2^32) family.
 """
 import argparse
 import os
@@ -15,6 +18,7 @@ def main():
     ap.add_argument("op", choices=["bfv_mul", "ckks_mul", "ckks_rot"])
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--openfhe-primes", action="store_true")
     args = ap.parse_args()
     import torch
     import herdsman_amd.backend as hb
@@ -22,7 +26,11 @@ def main():
     if args.op == "bfv_mul":
         c = hb.Context(hb.SCHEME_BFV, 15, 8, 4, 2, t=65537)
     else:
-        c = hb.Context(hb.SCHEME_CKKS, 16, 12, 4, 3)
+        mods = None
+        if args.openfhe_primes:
+            from herdsman_amd.params import openfhe_style_primes
+            mods = openfhe_style_primes([(60, 12), (61, 4)], 16)
+        c = hb.Context(hb.SCHEME_CKKS, 16, 12, 4, 3, moduli=mods)
     s = torch.cuda.current_stream()
     c.set_stream(s)
     shape = (args.batch, 2, c.L, c.n)
