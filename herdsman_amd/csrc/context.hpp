@@ -148,13 +148,14 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false,
 // with ksk [ndig][2][QP][N], formed in the last pass instead of read (EPI_KSQ)
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro = nullptr, const u64 *ext = nullptr,
-                           const u64 *ksk = nullptr, u32 ndig = 0);
+                           const u64 *ksk = nullptr, u32 ndig = 0, u32 base_g = 0);
 // ModUp of digit j fused into the column pass of the forward NTT of its
 // converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
 // the lazy (< 8q) NTT outputs times R
 int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j);
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n);
+// (base null: sigma(c0) is not stored; the combine then reads it with base_g)
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);
 // RNS kernels (rns.hip)

@@ -75,6 +75,7 @@ struct NttArgs {
   const u64 *e_pinv;     // [L] P^-1 R mod q_i
   u32 e_acc_stride;
   u32 e_add_mask;
+  u32 e_g;  // combine: 0, or the base is read as sigma_g(base) (rotation: sigma_g(c0) never stored)
   // EPI_KSQ (EPI_COMBINE whose acc_Q is the key-switching inner product, formed
   // here instead of being read): acc[p][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1,
   // p = 2 ct + b, with ext [ct][e_ndig][e_QP][N] and ksk [e_ndig][2][e_QP][N]
@@ -120,6 +121,17 @@ __host__ __device__ constexpr int ksq_digits(int e) { return e - EPI_KSQ + 1; }
 __host__ __device__ constexpr bool is_combine(int e) { return e == EPI_COMBINE || is_ksq(e); }
 
 // per-workgroup epilogue / prologue operands (resolved once per limb)
+// NTT-domain automorphism: slot k holds a(psi^e), e = 2 brv(k) + 1, and
+// sigma_g(a)(psi^e) = a(psi^(e g)); the byte offset of the source slot of k.
+// The 64 lanes of a coalesced load read one aligned 64-slot block of the
+// source (g only permutes inside it).
+template <int LOG_N>
+__device__ __forceinline__ u32 aut_src(u32 k, u32 g) {
+  constexpr u32 MASK = (2u << LOG_N) - 1;
+  const u32 e = (((__brev(k) >> (32 - LOG_N)) << 1) | 1) * g & MASK;
+  return (__brev(e >> 1) >> (32 - LOG_N)) << 3;
+}
+
 struct EpiRow {
   const u64 *acc;
   const u64 *kext, *kksk;  // EPI_KSQ: digit 0's ext / key row of this limb (digit j at + j stride)
@@ -130,7 +142,7 @@ struct EpiRow {
   bool add;
   const u64 *a0, *a1, *b0, *b1;  // PRO_TENSOR
   u64 *o0, *o1, *ext;
-  u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base; ext)
+  u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base or null; ext); combine: e_g
   u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is
   const u64 *src;  // PRO_CONV: source limb 0 of this poly (limb i at src + i N)
   u64 h[4];        // PRO_CONV: h[i][m] of this workgroup's target limb
@@ -359,7 +371,10 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if constexpr (EPI == EPI_COMBINE) pa[r] = ld_b(ep.acc + Grp<S, LOGR, 0>::k_reg(r), voff);
-        pb[r] = ep.add ? ld_b(ep.base + Grp<S, LOGR, 0>::k_reg(r), voff) : 0;
+        const u32 kr = Grp<S, LOGR, 0>::k_reg(r);
+        if (!ep.add) pb[r] = 0;
+        else if (ep.g) pb[r] = ld_b(ep.base, aut_src<LOG_N>((voff >> 3) + kr, ep.g));  // sigma_g(base)
+        else pb[r] = ld_b(ep.base + kr, voff);
       }
     }
     run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
@@ -563,33 +578,26 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         }
       }
     } else if constexpr (EPI == PRO_AUTOMORPH) {
-      // NTT-domain automorphism: slot k holds a(psi^e), e = 2 brv(k) + 1, and
-      // sigma_g(a)(psi^e) = a(psi^(e g)).  The 64 lanes of a load read one
-      // aligned 64-slot block of the source (g only permutes inside it).
-      // Software-pipelined like PRO_TENSOR: element r + PD's gathers are
-      // issued before element r's stores
-      constexpr u32 MASK = (2u << LOG_N) - 1;
+      // NTT-domain automorphism (aut_src), software-pipelined like PRO_TENSOR:
+      // element r + PD's gathers are issued before element r's stores.  With
+      // o0 null, sigma(c0) is not stored (the combine reads it as sigma_g(c0))
       constexpr int PD = AUT_PD;
-      const auto src_of = [&](int r) {
-        const u32 k = (voff >> 3) + GZ::k_reg(r);
-        const u32 e = (((__brev(k) >> (32 - LOG_N)) << 1) | 1) * ep.g & MASK;
-        return (__brev(e >> 1) >> (32 - LOG_N)) << 3;
-      };
+      const auto src_of = [&](int r) { return aut_src<LOG_N>((voff >> 3) + GZ::k_reg(r), ep.g); };
       u64 y[PD + 1][2];
 #pragma unroll
       for (int r = 0; r < PD; ++r) {
         const u32 sr = src_of(r);
-        y[r][0] = ld_b(ep.a0, sr), y[r][1] = ld_b(ep.a1, sr);
+        y[r][0] = ep.o0 ? ld_b(ep.a0, sr) : 0, y[r][1] = ld_b(ep.a1, sr);
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const u32 kr = GZ::k_reg(r);
         if (r + PD < R) {
           const u32 sn = src_of(r + PD);
-          y[(r + PD) % (PD + 1)][0] = ld_b(ep.a0, sn), y[(r + PD) % (PD + 1)][1] = ld_b(ep.a1, sn);
+          y[(r + PD) % (PD + 1)][0] = ep.o0 ? ld_b(ep.a0, sn) : 0, y[(r + PD) % (PD + 1)][1] = ld_b(ep.a1, sn);
         }
         const u64 y0 = y[r % (PD + 1)][0], y1 = y[r % (PD + 1)][1];
-        st_b(ep.o0 + kr, voff, y0);
+        if (ep.o0) st_b(ep.o0 + kr, voff, y0);
         x[r] = y1;
         st_b(ep.ext + kr, voff, csub(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
       }
@@ -750,6 +758,7 @@ __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NT
     ep.out = a.e_out + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
     ep.pinv = a.e_pinv[limb];
     ep.add = (a.e_add_mask >> (poly & 1)) & 1;
+    ep.g = a.e_g;
   }
   if constexpr (EPI == PRO_TENSOR) {
     const size_t LN = (size_t)a.t_L << LOG_N;
@@ -778,7 +787,7 @@ __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NT
     const size_t o = ((size_t)poly * 2 * a.t_L + limb) << LOG_N;
     ep.a0 = a.t_a + o;
     ep.a1 = ep.a0 + LN;
-    ep.o0 = a.t_out + o;
+    ep.o0 = a.t_out ? a.t_out + o : nullptr;
     ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
     ep.g = a.t_g;
   }
@@ -954,11 +963,13 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
 // With ext (EPI_KSQ, two-pass sizes) acc's Q limbs are not read: the last pass
 // forms acc[2 ct + b][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1 itself.
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
-                           u64 *out, u32 add_mask, const ConvTab *pro, const u64 *ext, const u64 *ksk, u32 ndig) {
+                           u64 *out, u32 add_mask, const ConvTab *pro, const u64 *ext, const u64 *ksk, u32 ndig,
+                           u32 base_g) {
   const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
   if (ext && (c->log_n <= 14 || ndig > 4 || (n_polys & 1)))
     return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch inner product: log_n / digits");
+  if (base_g && c->log_n <= 14) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated combine base: log_n");
   const u32 per = 65534u;  // gridDim.y, even (the polys of a ciphertext stay together)
   for (u32 p0 = 0; p0 < n_polys; p0 += per) {
     const u32 np = std::min(per, n_polys - p0);
@@ -974,6 +985,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
     a.e_pinv = c->d_pinv;
     a.e_acc_stride = acc_stride;
     a.e_add_mask = add_mask;
+    a.e_g = base_g & ((2u << c->log_n) - 1);
     if (ext) {
       a.e_ext = ext + (size_t)(p0 / 2) * ndig * QP * N;
       a.e_ksk = ksk;
@@ -1126,7 +1138,7 @@ int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *d
     t.ninv = c->d_ninv;
     t.log_n = c->log_n;
     t.t_a = ct + (size_t)p0 * 2 * L * N;
-    t.t_out = base + (size_t)p0 * 2 * L * N;
+    t.t_out = base ? base + (size_t)p0 * 2 * L * N : nullptr;
     t.t_ext = ext + (size_t)p0 * ndig * QP * N;
     t.t_L = L;
     t.t_QP = QP;

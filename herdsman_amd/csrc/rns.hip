@@ -614,8 +614,10 @@ static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
 // ext filled by ks_prep / the tensor INTT prologue / automorph_ks / the BEHZ floor).
 //   out : [n][2][L][N], out_b = (add_mask bit b ? base_b : 0) + KS(d)_b;
 //         base may alias out (element-wise).
+//   base_g (NTT form with the fused ModDown only): base_b is read as
+//         sigma_g(base_b); base must not overlap out.
 static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
-                         bool ntt_form, bool dc_is_coef = false) {
+                         bool ntt_form, bool dc_is_coef = false, u32 base_g = 0) {
   const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
   u64 *dc = w.dc, *ext = w.ext, *acc = w.acc, *conv = w.conv;
   int rc;
@@ -656,8 +658,9 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   if (ntt_form && c->fuse_moddown) {
     if ((rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale))) return rc;
     return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, &c->moddown, ksq ? ext : nullptr,
-                                  ksk, ndig);
+                                  ksk, ndig, base_g);
   }
+  if (base_g) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated key-switch base without the fused ModDown");
   // 5. ModDown: INTT the P part (all of Q u P for BFV), convert P -> Q
   if ((rc = ntt_launch(c, LimbMap{acc, QP, ntt_form ? K : QP, ntt_form ? L : 0, QP, 0, 0, 2 * n}, true,
                        ntt_form && c->fold_ninv)))
@@ -698,9 +701,14 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
   u64 *base = (u64 *)ws;  // [n][2][L][N], poly 0 = sigma(c0)
   const KsWs w = ks_layout(c, n, base + n * 2 * LN);
   if (ntt_form && c->log_n > 14) {
-    // CKKS at two-pass sizes: the automorphism runs inside the first pass of INTT(sigma(c1))
-    if ((rc = ntt_inv_automorph_launch(c, ct, g, base, w.dc, w.ext, n, w.ndig))) return rc;
-    return keyswitch_run(c, w, gk, base, out, n, 1u, true, true);
+    // CKKS at two-pass sizes: the automorphism runs inside the first pass of
+    // INTT(sigma(c1)).  With the fused ModDown and out apart from ct, sigma(c0)
+    // is never stored: the combine reads c0 through sigma_g itself
+    const u64 *ce = ct + (size_t)n * 2 * LN;
+    const bool apart = out + (size_t)n * 2 * LN <= ct || ce <= out;
+    const bool read_sigma = c->fuse_moddown && apart;
+    if ((rc = ntt_inv_automorph_launch(c, ct, g, read_sigma ? nullptr : base, w.dc, w.ext, n, w.ndig))) return rc;
+    return keyswitch_run(c, w, gk, read_sigma ? ct : base, out, n, 1u, true, true, read_sigma ? g : 0u);
   }
   if ((rc = SP_DISPATCH(c, automorph_ks_impl, c, ct, base, w.dc, w.ext, g, n, w.ndig, ntt_form))) return rc;
   return keyswitch_run(c, w, gk, base, out, n, 1u, ntt_form);

@@ -266,16 +266,30 @@ int main(int argc, char **argv) {
     const int schema = std::atoi(argv[5]);
     cfg.schemas = {parse_params(schema, argv[6])};
     if (const char *d = std::getenv("WG_DEVICE")) cfg.devices = {std::atoi(d)};
+    if (const char *v = std::getenv("WG_LANES")) cfg.lanes_per_device = (uint32_t)std::atoi(v);
+    if (const char *v = std::getenv("WG_MAX_BATCH")) cfg.max_batch = (uint32_t)std::atoi(v);
     GpuWorkerGroup g(cfg);
     Status st;
     if (mode == "map") {
-      herd::common::MapTask t;
-      t.session_uuid = {session};
-      t.input_data_frame_ptr.pointer = {{argv[7]}, (uint32_t)std::stoul(argv[8])};
-      t.output_data_frame_ptr = {{argv[9]}, (uint32_t)std::stoul(argv[8])};
-      t.crypto_key_ptr.schema_type = static_cast<herd::common::SchemaType>(schema);
-      t.circuit = parse_program(argc, argv, 10);
-      st = run(g, t);
+      // PART may list several partitions ("1,0"): one MapTask each, in order, on
+      // the same group (a failed task must leave its lane usable for the next)
+      int rc = 0;
+      std::string parts = argv[8];
+      for (size_t b = 0; b <= parts.size();) {
+        const size_t e = std::min(parts.find(',', b), parts.size());
+        const uint32_t part = (uint32_t)std::stoul(parts.substr(b, e - b));
+        herd::common::MapTask t;
+        t.session_uuid = {session};
+        t.input_data_frame_ptr.pointer = {{argv[7]}, part};
+        t.output_data_frame_ptr = {{argv[9]}, part};
+        t.crypto_key_ptr.schema_type = static_cast<herd::common::SchemaType>(schema);
+        t.circuit = parse_program(argc, argv, 10);
+        st = run(g, t);
+        std::printf("status: %s\n", name(st));
+        if (st != Status::COMPLETED) rc = 2;
+        b = e + 1;
+      }
+      return rc;
     } else if (mode == "reduce") {
       herd::common::ReduceTask t;
       t.session_uuid = {session};

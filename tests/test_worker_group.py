@@ -239,3 +239,31 @@ def test_gpu_bad_inputs_fail_the_task(wg_run, tmp_path):
                         "in0", "in1", "mul"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 2 and "status: ERROR" in r.stdout, r.stdout + r.stderr
     assert not os.path.exists(os.path.join(storage, "sy", "out2", "1"))
+
+
+@pytest.mark.gpu
+def test_gpu_failed_batch_leaves_the_lane_usable(wg_run, tmp_path):
+    """A bad row in a later batch of a task (one lane, one row per batch, so earlier
+    batches are still in flight on the lane's stream when it is read) fails that task
+    with Status::ERROR; the next task on the same lane reuses the staging buffers and
+    is bit-exact (the catch path synchronises the lane before completing)."""
+    from oracle_ffi import SCHEME_CKKS
+    o, storage, keys = _setup(tmp_path, SCHEME_CKKS, 12, 3, 2, 2)
+    rows = 3
+    a = o.uniform((rows, 2, o.L, o.n), seed=51)
+    b = o.uniform((rows, 2, o.L, o.n), seed=52)
+    rlk = o.uniform(o.key_shape(), seed=53)
+    good = [ct_row(o, [a[i], b[i]]) for i in range(rows)]
+    bad = bytearray(good[2])
+    bad[0:4] = struct.pack("<I", 0xDEADBEEF)  # corrupt the CtHeader magic of the third row
+    write_partition(os.path.join(storage, "sl", "in", "1"), good[:2] + [bytes(bad)])
+    write_partition(os.path.join(storage, "sl", "in", "0"), good)
+    write_keys(os.path.join(keys, "sl", "0.key"), o, rlk, {})
+    env = dict(os.environ, WG_LANES="1", WG_MAX_BATCH="1")
+    r = subprocess.run([wg_run, "map", storage, keys, "sl", "0", params_arg(o, str(tmp_path)), "in", "1,0", "out",
+                        "in0", "in1", "mul"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert r.stdout.split("status: ")[1:] == ["ERROR\n", "COMPLETED\n"], r.stdout + r.stderr
+    assert not os.path.exists(os.path.join(storage, "sl", "out", "1"))
+    got = np.stack([parse_row(o, p) for p in read_partition(os.path.join(storage, "sl", "out", "0"))])
+    assert np.array_equal(got, o.mul_relin(a, b, rlk))
