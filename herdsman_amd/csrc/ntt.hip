@@ -113,14 +113,19 @@ struct NttArgs {
 // EPI_KSQ + d - 1: EPI_COMBINE with the Q limbs' key-switching inner product
 // over d = 1..4 digits fused in (the digit count is compile-time)
 // PRO_CONV + ns - 1: the conversion prologue over ns = 1..4 source limbs (compile-time)
-enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, EPI_KSQ = 6, PRO_CONV = 11 };
+// PRO_KSP + d - 1: prologue of the inverse first (row) pass of INTT(acc_P):
+// the P limbs' key-switching inner product over d = 1..4 digits (acc_P is
+// formed at the load positions and never stored)
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, EPI_KSQ = 6, PRO_CONV = 11,
+       PRO_KSP = 16 };
 __host__ __device__ constexpr bool is_conv(int e) { return e >= PRO_CONV && e < PRO_CONV + 4; }
 __host__ __device__ constexpr int conv_ns(int e) { return e - PRO_CONV + 1; }
 __host__ __device__ constexpr bool is_ksq(int e) { return e >= EPI_KSQ && e < EPI_KSQ + 4; }
 __host__ __device__ constexpr int ksq_digits(int e) { return e - EPI_KSQ + 1; }
 __host__ __device__ constexpr bool is_combine(int e) { return e == EPI_COMBINE || is_ksq(e); }
+__host__ __device__ constexpr bool is_ksp(int e) { return e >= PRO_KSP && e < PRO_KSP + 4; }
+__host__ __device__ constexpr int ksp_digits(int e) { return e - PRO_KSP + 1; }
 
-// per-workgroup epilogue / prologue operands (resolved once per limb)
 // NTT-domain automorphism: slot k holds a(psi^e), e = 2 brv(k) + 1, and
 // sigma_g(a)(psi^e) = a(psi^(e g)); the byte offset of the source slot of k.
 // The 64 lanes of a coalesced load read one aligned 64-slot block of the
@@ -132,9 +137,10 @@ __device__ __forceinline__ u32 aut_src(u32 k, u32 g) {
   return (__brev(e >> 1) >> (32 - LOG_N)) << 3;
 }
 
+// per-workgroup epilogue / prologue operands (resolved once per limb)
 struct EpiRow {
   const u64 *acc;
-  const u64 *kext, *kksk;  // EPI_KSQ: digit 0's ext / key row of this limb (digit j at + j stride)
+  const u64 *kext, *kksk;  // EPI_KSQ, PRO_KSP: digit 0's ext / key row of this limb (digit j at + j stride)
   size_t ext_j, ksk_j;     // digit strides (words)
   const u64 *base;
   u64 *out;
@@ -601,6 +607,53 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         x[r] = y1;
         st_b(ep.ext + kr, voff, csub(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
       }
+    } else if constexpr (is_ksp(EPI)) {
+      // acc_P = sum_j ext_j ksk_j R^-1 (ks_inner_kernel; ext carries R) at the
+      // coalesced positions, canonical: the products are below 1.5q (2q
+      // generic), the running sum is kept below 2q.  Operands software-
+      // pipelined PD elements deep (as EPI_KSQ)
+      constexpr int KD = ksp_digits(EPI);
+      constexpr int PD = SP ? 2 : 1;
+      u64 nq1 = 0 - mi.q, nq2 = 0 - 2 * mi.q;
+      asm("" : "+s"(nq1));
+      asm("" : "+s"(nq2));
+      u64 ek[PD + 1][2 * KD];
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        const u32 kr = GZ::k_reg(r);
+#pragma unroll
+        for (int j = 0; j < KD; ++j) {
+          ek[r][j] = ld_b(ep.kext + j * ep.ext_j + kr, voff);
+          ek[r][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r + PD < R) {
+          const u32 kn = GZ::k_reg(r + PD);
+#pragma unroll
+          for (int j = 0; j < KD; ++j) {
+            ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + j * ep.ext_j + kn, voff);
+            ek[(r + PD) % (PD + 1)][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
+          }
+        }
+        u64 e[KD], k[KD], pr[KD];
+#pragma unroll
+        for (int j = 0; j < KD; ++j) {
+          e[j] = ek[r % (PD + 1)][j];
+          k[j] = ek[r % (PD + 1)][KD + j];
+        }
+        if constexpr (SP) {
+          mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+        } else {
+#pragma unroll
+          for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
+        }
+        u64 acc = pr[0];
+#pragma unroll
+        for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
+        x[r] = harvey_csub(acc, nq1);
+      }
     } else {
 #pragma unroll
       for (int r = 0; r < R; ++r) x[r] = ld_d(data + GZ::k_reg(r), voff);
@@ -667,11 +720,11 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int WM>
 __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NTT_MINW : 1) ntt_pass(NttArgs a) {
   static_assert(is_combine(EPI) || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
-                    EPI == PRO_BFVT || is_conv(EPI),
+                    EPI == PRO_BFVT || is_conv(EPI) || is_ksp(EPI),
                 "ntt_pass epilogues");
   static_assert(!is_conv(EPI) || (!INV && COLS), "the conversion prologue feeds a forward column pass");
   static_assert(!is_combine(EPI) || (!INV && !COLS), "epilogues follow a forward row pass");
-  static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT) || (INV && !COLS),
+  static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT && !is_ksp(EPI)) || (INV && !COLS),
                 "prologues feed an inverse row pass");
   using PG = PassGeo<LOG_N, S, COLS, INV>;
   static_assert(!is_combine(EPI) || PG::LAST, "epilogues run in the last pass");
@@ -699,7 +752,7 @@ __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NT
       act = j / gridDim.y;
     }
   }
-  if constexpr (is_ksq(EPI)) {
+  if constexpr (is_ksq(EPI) || is_ksp(EPI)) {
     // the 2 n polys (ct, b) of one (limb, row block) on consecutive workgroup
     // ids of ONE XCD: the limb's key rows (2 dnum of them) stay in that XCD's
     // L2 for the whole batch, and the b = 1 item re-reads the ext rows the
@@ -745,6 +798,13 @@ __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NT
   const u32 gb = (hi << (S + PG::LS)) + (u & (stride - 1));
 
   EpiRow ep{};
+  if constexpr (is_ksp(EPI)) {
+    const size_t N = (size_t)1 << LOG_N;
+    ep.ext_j = (size_t)a.e_QP * N;
+    ep.ksk_j = 2 * ep.ext_j;
+    ep.kext = a.e_ext + ((size_t)(poly >> 1) * a.e_ndig * a.e_QP + limb) * N;
+    ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_QP + limb) * N;
+  }
   if constexpr (is_combine(EPI)) {
     if constexpr (is_ksq(EPI)) {
       const size_t N = (size_t)1 << LOG_N;
@@ -847,7 +907,7 @@ int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
     return c->special ? launch_fwd<LOG_N, S, W, COLS, EPI, true>(c, a, n_jobs)
                       : launch_fwd<LOG_N, S, W, COLS, EPI, false>(c, a, n_jobs);
-  } else if constexpr (EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH || EPI == PRO_BFVT) {
+  } else if constexpr (EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH || EPI == PRO_BFVT || is_ksp(EPI)) {
     if (!inv) return fhe_fail(c, FHE_ERR_INVALID, "prologue on a forward pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
                       : launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs);
@@ -1150,6 +1210,44 @@ int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *d
     int rc;
     if ((rc = row_pass<PRO_AUTOMORPH>(c, t, true, np * L))) return rc;
     if ((rc = col_pass(c, t, true, np * L))) return rc;
+  }
+  return FHE_OK;
+}
+
+// INTT of the P limbs of the key-switching accumulator acc [2n][QP][N], with
+// their inner product acc_P[2 ct + b][k] = sum_j ext[ct][j][k] ksk[j][b][k] R^-1
+// (ks_inner_kernel) formed in the first (row) pass (PRO_KSP): acc_P is never
+// stored, the P rows of acc receive INTT(acc_P) times d_iscale (ModDown's
+// source constants, as ntt_launch(..., d_iscale) gives them)
+int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig) {
+  const u32 L = c->L, K = c->K, QP = L + K;
+  const size_t N = c->n;
+  if (c->log_n <= 14 || ndig < 1 || ndig > 4)
+    return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused P-limb inner product: log_n / digits");
+  const u32 per = 65534u;  // gridDim.y, even (the polys of a ciphertext stay together)
+  for (u32 p0 = 0; p0 < 2 * n; p0 += per) {
+    const u32 np = std::min(per, 2 * n - p0);
+    NttArgs a{};
+    a.map = LimbMap{acc + (size_t)p0 * QP * N, QP, K, L, QP, 0, 0, np};
+    a.tw = c->d_tw_inv;
+    a.mods = c->d_mods;
+    a.ninv = c->d_ninv;
+    a.log_n = c->log_n;
+    a.scale = c->d_iscale;
+    a.e_ext = ext + (size_t)(p0 / 2) * ndig * QP * N;
+    a.e_ksk = ksk;
+    a.e_ndig = ndig;
+    a.e_QP = QP;
+    const u32 n_jobs = np * K;
+    int rc;
+    switch (ndig) {
+      case 1: rc = row_pass<PRO_KSP>(c, a, true, n_jobs); break;
+      case 2: rc = row_pass<PRO_KSP + 1>(c, a, true, n_jobs); break;
+      case 3: rc = row_pass<PRO_KSP + 2>(c, a, true, n_jobs); break;
+      default: rc = row_pass<PRO_KSP + 3>(c, a, true, n_jobs); break;
+    }
+    if (rc) return rc;
+    if ((rc = col_pass(c, a, true, n_jobs))) return rc;
   }
   return FHE_OK;
 }

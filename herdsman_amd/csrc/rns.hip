@@ -599,6 +599,9 @@ struct KsWs {
   u64 *dc, *ext, *acc, *conv;
   u32 ndig;
 };
+#ifndef KSP_FUSE
+#define KSP_FUSE 1  // the P limbs' inner product inside INTT(acc_P)'s first pass (0: ks_inner_kernel)
+#endif
 static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
   const size_t L = c->L, QP = c->L + c->K, N = c->n;
   KsWs w;
@@ -649,14 +652,19 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   //    digits, the Q limbs' inner product runs inside the last pass of
   //    NTT(conv) (EPI_KSQ), so only the P limbs (ModDown's sources) are formed
   //    here: acc_Q is never written and read back
+  //    The P limbs' inner product runs likewise inside the first pass of
+  //    INTT(acc_P) (PRO_KSP): no ks_inner_kernel at all
   const bool ksq = ntt_form && c->fuse_moddown && ndig <= 4;
-  if ((rc = SP_DISPATCH(c, inner_impl, c, ext, ksk, acc, n, ndig, ksq ? L : 0, ksq ? K : QP))) return rc;
+  if (!(ksq && KSP_FUSE) && (rc = SP_DISPATCH(c, inner_impl, c, ext, ksk, acc, n, ndig, ksq ? L : 0, ksq ? K : QP)))
+    return rc;
   // 5-6. ModDown for NTT-form results: INTT the P part with the conversion's
   //      source constants as its output scale, then NTT(conv) with the P -> Q
   //      conversion in its first pass and the combine in its last
   //      (out = base + (acc_Q - conv) P^-1): conv never makes an HBM round trip
   if (ntt_form && c->fuse_moddown) {
-    if ((rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale))) return rc;
+    if (ksq && KSP_FUSE) rc = ntt_inv_ksp_launch(c, acc, ext, ksk, n, ndig);
+    else rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale);
+    if (rc) return rc;
     return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, &c->moddown, ksq ? ext : nullptr,
                                   ksk, ndig, base_g);
   }
