@@ -36,6 +36,9 @@
 #ifndef KSQ_PD
 #define KSQ_PD 2  // EPI_KSQ operand prefetch depth (elements; 3 measured no faster, profiles/r03/ab_ksq_pd_aut.txt)
 #endif
+#ifndef KSP_PD
+#define KSP_PD 2  // PRO_KSP operand prefetch depth (elements)
+#endif
 #ifndef AUT_PD
 #define AUT_PD 2  // PRO_AUTOMORPH gather prefetch depth (elements)
 #endif
@@ -613,7 +616,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       // generic), the running sum is kept below 2q.  Operands software-
       // pipelined PD elements deep (as EPI_KSQ)
       constexpr int KD = ksp_digits(EPI);
-      constexpr int PD = SP ? 2 : 1;
+      constexpr int PD = SP ? KSP_PD : 1;
       u64 nq1 = 0 - mi.q, nq2 = 0 - 2 * mi.q;
       asm("" : "+s"(nq1));
       asm("" : "+s"(nq2));
