@@ -36,6 +36,18 @@
 #ifndef KSQ_PD
 #define KSQ_PD 2  // EPI_KSQ operand prefetch depth (elements; 3 measured no faster, profiles/r03/ab_ksq_pd_aut.txt)
 #endif
+#ifndef TENSOR_CHUNK
+#define TENSOR_CHUNK 65535u  // ciphertexts per INTT(d2) pass pair (MALL-sized chunks: see DESIGN §4)
+#endif
+#ifndef COMBINE_CHUNK
+#define COMBINE_CHUNK 65534u  // polys per NTT(conv) pass pair (even)
+#endif
+#ifndef KSQ_GI
+#define KSQ_GI 1  // EPI_KSQ: (limb, row block) groups interleaved per XCD (4: kernel -1.6% but headline -0.2%, profiles/r03/ab_group_interleave.txt)
+#endif
+#ifndef KSP_GI
+#define KSP_GI 1  // PRO_KSP: the same
+#endif
 #ifndef KSP_PD
 #define KSP_PD 2  // PRO_KSP operand prefetch depth (elements)
 #endif
@@ -760,9 +772,14 @@ __global__ void __launch_bounds__(W << (S - LOGR), (W << (S - LOGR)) == 256 ? NT
     // ids of ONE XCD: the limb's key rows (2 dnum of them) stay in that XCD's
     // L2 for the whole batch, and the b = 1 item re-reads the ext rows the
     // b = 0 item just fetched
+    // GI groups are interleaved per XCD (their key rows all L2-resident)
+    constexpr u32 GIW = is_ksq(EPI) ? KSQ_GI : KSP_GI;
     const u32 np = gridDim.y, lin = blockIdx.x + gridDim.x * (blockIdx.y + np * blockIdx.z);
-    const u32 r = lin >> 3, g = (r / np) * 8 + (lin & 7);  // g = (limb, row block)
-    poly = r % np;
+    const u32 r = lin >> 3, gpx = gridDim.x * gridDim.z / 8;  // groups per XCD
+    const u32 GI = gpx % GIW == 0 ? GIW : 1;
+    const u32 within = r % (GI * np);
+    const u32 g = ((r / (GI * np)) * GI + within % GI) * 8 + (lin & 7);  // g = (limb, row block)
+    poly = within / GI;
     bx = g % gridDim.x;
     act = g / gridDim.x;
   }
@@ -1033,7 +1050,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
   if (ext && (c->log_n <= 14 || ndig > 4 || (n_polys & 1)))
     return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch inner product: log_n / digits");
   if (base_g && c->log_n <= 14) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated combine base: log_n");
-  const u32 per = 65534u;  // gridDim.y, even (the polys of a ciphertext stay together)
+  const u32 per = COMBINE_CHUNK;  // polys per pass pair: gridDim.y, even (the polys of a ciphertext stay together)
   for (u32 p0 = 0; p0 < n_polys; p0 += per) {
     const u32 np = std::min(per, n_polys - p0);
     NttArgs a{};
@@ -1149,7 +1166,7 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig) {
   const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
-  const u32 per = 65535u;  // gridDim.y
+  const u32 per = TENSOR_CHUNK;  // ciphertexts per pass pair (gridDim.y <= 65535)
   for (u32 p0 = 0; p0 < n; p0 += per) {
     const u32 np = std::min(per, n - p0);
     NttArgs t{};
