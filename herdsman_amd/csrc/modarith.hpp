@@ -209,6 +209,19 @@ HD u64 mont_mul(u64 a, u64 b, const ModInfo &m) {  // a*b*2^-64, [0,2q); a < 2^6
 }
 
 HD u64 csub(u64 a, u64 q) { return a >= q ? a - q : a; }
+// the same for a, q < 2^63: the sign of a - q selects (a 64-bit add, a shift
+// and two bitfield selects instead of a quarter-rate 64-bit compare, a borrow
+// chain and two selects behind an s_nop hazard)
+HD u64 csub63(u64 a, u64 q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const u64 d = a - q;
+  const u32 m = (u32)((int32_t)(u32)(d >> 32) >> 31);  // all ones iff a < q
+  const u64 mm = ((u64)m << 32) | m;
+  return (a & mm) | (d & ~mm);
+#else
+  return a >= q ? a - q : a;
+#endif
+}
 HD u64 add_mod(u64 a, u64 b, u64 q) { return csub(a + b, q); }
 HD u64 sub_mod(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
 
@@ -242,7 +255,7 @@ HD u64 dot_mont(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModIn
 #pragma unroll
         for (int i = c0; i < c0 + 4 && i < NS; ++i)
           if (i < (int)ns) sum += mont_mul<SP>(v[i], h[(size_t)i * hs], m);
-        part = csub(csub(csub(sum, 4 * m.q), 2 * m.q), m.q);
+        part = csub63(csub63(csub(sum, 4 * m.q), 2 * m.q), m.q);  // sum < 6q may exceed 2^63
       } else {
         U128 acc{0, 0};
 #pragma unroll
@@ -250,7 +263,7 @@ HD u64 dot_mont(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModIn
           if (i < (int)ns) mac128(acc, v[i], h[(size_t)i * hs]);
         part = csub(mont_reduce<SP>(acc, m), m.q);
       }
-      res = c0 == 0 ? part : add_mod(res, part, m.q);
+      res = c0 == 0 ? part : csub63(res + part, m.q);  // both canonical
     }
   }
   return res;

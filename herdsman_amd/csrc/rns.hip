@@ -343,7 +343,9 @@ struct BehzDev {
 };
 
 // behz_extend (oracle): fastbconv_m_tilde then sm_mrq.  x [L] coef -> [nB] coef
-template <int NL, bool SP>
+// EX: L == NL exactly (nB = L + 1 always), so every loop is unrolled with no
+// per-limb guards (the C3 parameters); otherwise NL bounds L.
+template <int NL, bool SP, bool EX>
 // Poly p = 4 item + w of the BFV product's operands (w: a0, a1, b0, b1) is
 // read straight from the ciphertexts and extended to Bsk in xb [2][n][2][nB][N]
 // (the a and b parts, each in the ciphertexts' own layout).  The Q part is not
@@ -354,28 +356,32 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 p = blockIdx.y, item = p >> 2, w = p & 3;
   const size_t N = (size_t)1 << log_n;
-  const u32 L = bz->L, nB = bz->nB;
+  const u32 L = EX ? NL : bz->L, nB = L + 1;
   const u64 *s = (w < 2 ? a : b) + ((size_t)(2 * item + (w & 1)) * L) * N + k;
   u64 v[NL];
   u32 xmt = 0;
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     v[i] = 0;
-    if (i < (int)L) {
+    if (EX || i < (int)L) {
       const ModInfo m = mods[i];
       const u64 x = ld_nt(s + i * N);
-      v[i] = csub(mont_mul<SP>(x, bz->mt_hinv_R[i], m), m.q);
+      v[i] = csub63(mont_mul<SP>(x, bz->mt_hinv_R[i], m), m.q);
       xmt += (u32)v[i] * bz->h_mod_mt[i];
     }
   }
   const u32 r = xmt * bz->neg_inv_q_mod_mt;
   u64 *d = xb + ((size_t)((w >> 1) * n_items + item) * 2 + (w & 1)) * nB * N + k;
-  for (u32 j = 0; j < nB; ++j) {
-    const ModInfo m = mods[bz->bsk0 + j];
-    // (sum_i v_i (Q/q_i) + r Q) 2^-32, the 2^-32 folded into the weights
-    const u64 xbj = dot_mont<NL, SP>(v, &bz->hx_R[0][j], BEHZ_MAXL + 1, L, m);
-    const u64 rr = r >= 0x80000000u ? (u64)r + m.q - (1ull << 32) : (u64)r;   // centered r mod b
-    d[j * N] = add_mod(xbj, csub(mont_mul<SP>(rr, bz->qx_R[j], m), m.q), m.q);
+  constexpr int UJ = EX ? NL + 1 : 1;  // unrolled only with compile-time bounds
+#pragma unroll UJ
+  for (int j = 0; j < NL + 1; ++j) {
+    if (EX || j < (int)nB) {
+      const ModInfo m = mods[bz->bsk0 + j];
+      // (sum_i v_i (Q/q_i) + r Q) 2^-32, the 2^-32 folded into the weights
+      const u64 xbj = dot_mont<NL, SP>(v, &bz->hx_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 rr = r >= 0x80000000u ? (u64)r + m.q - (1ull << 32) : (u64)r;   // centered r mod b
+      d[j * N] = csub63(xbj + csub63(mont_mul<SP>(rr, bz->qx_R[j], m), m.q), m.q);
+    }
   }
 }
 
@@ -383,7 +389,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
 // The third output r2 goes straight into the key-switch scratch (the KS
 // preparation of ks_prep_kernel fused here): dc = r2 and the own-digit ext
 // slot = r2 R, so r2 is not written and read back by a separate kernel.
-template <int NL, bool SP>
+template <int NL, bool SP, bool EX>
 __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restrict__ eq, const u64 *__restrict__ eb,
                                                               u64 *__restrict__ out01, u64 *__restrict__ dc,
                                                               u64 *__restrict__ ext, const BehzDev *bz,
@@ -392,16 +398,16 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 ct = blockIdx.y / 3, p = blockIdx.y % 3;
   const size_t N = (size_t)1 << log_n;
-  const u32 L = bz->L, nB = bz->nB;
+  const u32 L = EX ? NL : bz->L, nB = L + 1;
   const u64 *xq = eq + ((size_t)(ct * 3 + p) * L) * N + k;
   const u64 *xb = eb + ((size_t)(ct * 3 + p) * nB) * N + k;
   u64 v[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     v[i] = 0;
-    if (i < (int)L) {
+    if (EX || i < (int)L) {
       const ModInfo m = mods[i];
-      v[i] = csub(mont_mul<SP>(xq[i * N], bz->t_hinv_R[i], m), m.q);  // [t x (Q/q_i)^-1]_{q_i}
+      v[i] = csub63(mont_mul<SP>(xq[i * N], bz->t_hinv_R[i], m), m.q);  // [t x (Q/q_i)^-1]_{q_i}
     }
   }
   // fast_floor: ((t x)_b - conv_Q->b(t x)) * Q^-1, then the fastbconv_sk
@@ -411,11 +417,11 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   u64 flsk = 0;
 #pragma unroll
   for (int j = 0; j < NL + 1; ++j) {
-    if (j < (int)nB) {
+    if (EX || j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
       const u64 cv = dot_mont<NL, SP>(v, &bz->hf_R[0][j], BEHZ_MAXL + 1, L, m);
-      const u64 tx = csub(mont_mul<SP>(xb[j * N], bz->tf_R[j], m), m.q);
-      const u64 wj = add_mod(tx, cv, m.q);
+      const u64 tx = csub63(mont_mul<SP>(xb[j * N], bz->tf_R[j], m), m.q);
+      const u64 wj = csub63(tx + cv, m.q);
       if (j == (int)nB - 1) flsk = wj;
       else if (j < NL) w[j] = wj;
     } else if (j < NL) {
@@ -427,13 +433,13 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   const bool neg = alpha > msk.q / 2;
   const u64 amag = neg ? msk.q - alpha : alpha;
   u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
-  for (u32 i = 0; i < L; ++i) {
+  for (int i = 0; i < (EX ? NL : (int)L); ++i) {
     const ModInfo m = mods[i];
     const u64 cq = dot_mont<NL, SP>(w, &bz->h_b_q_R[0][i], BEHZ_MAXL, nB - 1, m);
-    const u64 ab = csub(mont_mul<SP>(amag, bz->b_mod_q_R[i], m), m.q);
-    const u64 r = neg ? add_mod(cq, ab, m.q) : sub_mod(cq, ab, m.q);
+    const u64 ab = csub63(mont_mul<SP>(amag, bz->b_mod_q_R[i], m), m.q);
+    const u64 r = csub63(cq + (neg ? ab : m.q - ab), m.q);  // cq -/+ ab (ab = 0 gives cq + q -> cq)
     o[i * N] = r;
-    if (p == 2) ext[((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k] = csub(mont_mul<SP>(r, m.r2, m), m.q);
+    if (p == 2) ext[((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k] = csub63(mont_mul<SP>(r, m.r2, m), m.q);
   }
 }
 
@@ -524,9 +530,10 @@ template <bool SP>
 int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
   dim3 grid(c->n / EW_BLOCK, 4 * n);
   const BehzDev *bz = (const BehzDev *)c->behz;
-  if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
-  else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
-  else hipLaunchKernelGGL((behz_extend_kernel<24, SP>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  if (c->L == 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  else if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  else hipLaunchKernelGGL((behz_extend_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
   return fhe_check(c, hipGetLastError(), "behz_extend");
 }
 
@@ -535,9 +542,10 @@ int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *d
   dim3 grid(c->n / EW_BLOCK, n * 3);
   const BehzDev *bz = (const BehzDev *)c->behz;
   const u32 QP = c->L + c->K;
-  if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
-  else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
-  else hipLaunchKernelGGL((behz_floor_kernel<24, SP>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  if (c->L == 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  else if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  else hipLaunchKernelGGL((behz_floor_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
   return fhe_check(c, hipGetLastError(), "behz_floor");
 }
 

@@ -18,8 +18,8 @@ def main():
         stats[v] = {}
         for r in csv.DictReader(open(f"{out}/{v}/run_kernel_stats.csv")):
             n = r["Name"]
-            n = n[n.find("ntt_pass"):] if "ntt_pass" in n else n
-            n = n.split("((")[0].split("(anonymous")[0]
+            n = n.replace("(anonymous namespace)::", "").replace("void ", "")
+            n = n.split("(")[0]
             stats[v][n] = float(r["AverageNs"]) / 1e3
     names = sorted(stats[rest[0]], key=lambda n: -stats[rest[0]][n])
     print(f"{'kernel (avg us)':60s} " + " ".join(f"{v:>9s}" for v in rest))
