@@ -273,7 +273,9 @@ HD u64 dot_mont(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModIn
 // (generic) -- the input range of the forward NTT (ntt.hip), so a conversion
 // whose outputs are transformed next skips the last two (one) conditional
 // subtractions; the residue is the same, the NTT's outputs are bit-identical.
-template <int NS, bool SP>
+// Q60: m < 2^60, so the lazy sums (< 8q) stay below 2^63 and the conditional
+// subtractions can use the sign of a - q (csub63)
+template <int NS, bool SP, bool Q60 = false>
 HD u64 dot_mont_lazy(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
   u64 res = 0;
 #pragma unroll
@@ -285,8 +287,8 @@ HD u64 dot_mont_lazy(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const 
 #pragma unroll
         for (int i = c0; i < c0 + 4 && i < NS; ++i)
           if (i < (int)ns) sum += mont_mul<SP>(v[i], h[(size_t)i * hs], m);
-        part = csub(sum, 4 * m.q);  // < 4q
-        res = c0 == 0 ? part : csub(res + part, 4 * m.q);
+        part = Q60 ? csub63(sum, 4 * m.q) : csub(sum, 4 * m.q);  // < 4q
+        res = c0 == 0 ? part : Q60 ? csub63(res + part, 4 * m.q) : csub(res + part, 4 * m.q);
       } else {
         U128 acc{0, 0};
 #pragma unroll

@@ -620,7 +620,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         const u64 y0 = y[r % (PD + 1)][0], y1 = y[r % (PD + 1)][1];
         if (ep.o0) st_b(ep.o0 + kr, voff, y0);
         x[r] = y1;
-        st_b(ep.ext + kr, voff, csub(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
+        st_b(ep.ext + kr, voff, csub63(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
       }
     } else if constexpr (is_ksp(EPI)) {
       // acc_P = sum_j ext_j ksk_j R^-1 (ks_inner_kernel; ext carries R) at the
@@ -702,7 +702,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
           for (int i = 0; i < NS; ++i)
             sv[j][i] = ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont_lazy<NS, SP>(sv[j], ep.h, 1, NS, mi);  // < 4q
+        for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);  // < 4q
       }
     } else {
       // the first forward pass may read out of place (NttArgs::src)

@@ -117,7 +117,7 @@ __device__ __forceinline__ void conv_scale(u64 (&v)[CONV_CPT][NS], const u64 (&x
     const ModInfo ms = mods[src_mod ? src_mod[on ? i : 0] : mod0 + (on ? i : 0)];
     const u64 hv = t.hinv[on ? i : 0];
 #pragma unroll
-    for (int c = 0; c < CONV_CPT; ++c) v[c][i] = on ? csub(mont_mul<SP>(x[c][i], hv, ms), ms.q) : 0;
+    for (int c = 0; c < CONV_CPT; ++c) v[c][i] = on ? csub63(mont_mul<SP>(x[c][i], hv, ms), ms.q) : 0;
   }
 }
 
@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_prep_kernel(const u64 *__restrict
   const ModInfo m = mods[i];
   const u64 x = d[((size_t)ct * d_stride + i) * N + k];
   dc[((size_t)ct * L + i) * N + k] = x;
-  ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub(mont_mul<SP>(x, m.r2, m), m.q);
+  ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub63(mont_mul<SP>(x, m.r2, m), m.q);
 }
 
 // KS inner product (keyswitch_one, oracle):
@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_combine_kernel(const u64 *__restr
   const ModInfo m = mods[i];
   const u64 a = acc[((size_t)(2 * ct + b) * QP + i) * N + k];
   const u64 cv = conv[((size_t)(2 * ct + b) * L + i) * N + k];
-  u64 ks = csub(mont_mul<SP>(sub_mod(a, cv, m.q), pinv[i], m), m.q);
+  u64 ks = csub63(mont_mul<SP>(sub_mod(a, cv, m.q), pinv[i], m), m.q);
   const size_t o = ((size_t)(2 * ct + b) * L + i) * N + k;
   if (add_mask & (1u << b)) ks = add_mod(ks, base[o], m.q);
   out[o] = ks;
@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(EW_BLOCK) automorph_ks_kernel(const u64 *__res
   }
   base[(size_t)ct * 2 * LN + (size_t)i * N + k] = y0;
   dc[(size_t)ct * LN + (size_t)i * N + k] = y1;
-  ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub(mont_mul<SP>(y1, m.r2, m), m.q);
+  ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub63(mont_mul<SP>(y1, m.r2, m), m.q);
 }
 
 // ----------------------------------------------------------------- BEHZ
