@@ -302,6 +302,63 @@ HD u64 dot_mont_lazy(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const 
   return res;
 }
 
+// NS <= 4 canonical terms v_i < 2^61 (constants h_i < m < 2^61): the same
+// sum as dot_mont_lazy by 31-bit column sums.  With v = v0 + v1 2^31
+// (v0 < 2^31, v1 < 2^30: an and and a funnel shift) and h = h0 + h1 2^31 (split
+// once per workgroup, uniform), every 32x32 partial product is below 2^62, so
+// the three columns  C0 = sum v0 h0,  C1 = sum v0 h1 + v1 h0,  C2 = sum v1 h1
+// accumulate in the 64-bit addend of v_mad_u64_u32 with no carries: 4 multiply-
+// adds per term instead of the Montgomery product's 6 plus its lazy-sum adds
+// and conditional subtractions.  T = C0 + C1 2^31 + C2 2^62 < 2^63 m is then
+// reduced once (mont_reduce: [0, 2q); generic moduli save the 128-bit
+// accumulation's carry chains).
+template <int NS, bool SP>
+HD u64 dot_cols(const u64 (&v)[NS], const u32 (&h0)[NS], const u32 (&h1)[NS], const ModInfo &m) {
+  static_assert(NS >= 1 && NS <= 4, "column sums stay below 2^64 for at most 4 terms");
+  u64 c0 = 0, c1 = 0, c2 = 0;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const u32 v0 = (u32)v[i] & 0x7FFFFFFFu, v1 = (u32)(v[i] >> 31);
+    c0 += (u64)v0 * h0[i];
+    c1 += (u64)v0 * h1[i];
+    c1 += (u64)v1 * h0[i];
+    c2 += (u64)v1 * h1[i];
+  }
+  const u64 lo1 = c0 + (c1 << 31);
+  const u64 lo = lo1 + (c2 << 62);
+  const u64 hi = (c1 >> 33) + (c2 >> 2) + (lo1 < c0) + (lo < lo1);
+  return mont_reduce<SP>(U128{lo, hi}, m);
+}
+HD void split31(u64 h, u32 &h0, u32 &h1) {
+  h0 = (u32)h & 0x7FFFFFFFu;
+  h1 = (u32)(h >> 31);
+}
+
+// dot_mont's canonical sum (same arguments) by column sums over chunks of 4
+// terms, each reduced once; constants are split where they are read (uniform
+// operands: scalar instructions).  Terms past ns contribute zero digits.
+template <int NS, bool SP>
+HD u64 dot_cols_canon(const u64 (&v)[NS], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
+  u64 res = 0;
+#pragma unroll
+  for (int c0 = 0; c0 < NS; c0 += 4) {
+    if (c0 < (int)ns) {
+      u64 vv[4];
+      u32 h0[4], h1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool on = c0 + i < NS && c0 + i < (int)ns;
+        vv[i] = on ? v[c0 + i < NS ? c0 + i : 0] : 0;
+        if (on) split31(h[(size_t)(c0 + i) * hs], h0[i], h1[i]);
+        else h0[i] = h1[i] = 0;
+      }
+      const u64 part = csub63(dot_cols<4, SP>(vv, h0, h1, m), m.q);
+      res = c0 == 0 ? part : csub63(res + part, m.q);
+    }
+  }
+  return res;
+}
+
 // SplitMix64 stream shared with the oracle (orc_fill_uniform)
 HD u64 splitmix64(u64 z) {
   z ^= z >> 30;

@@ -51,6 +51,9 @@
 #ifndef KSP_PD
 #define KSP_PD 2  // PRO_KSP operand prefetch depth (elements)
 #endif
+#ifndef CONV_COLS
+#define CONV_COLS 1  // PRO_CONV: 31-bit column sums (dot_cols); 0: dot_mont_lazy
+#endif
 #ifndef AUT_PD
 #define AUT_PD 2  // PRO_AUTOMORPH gather prefetch depth (elements)
 #endif
@@ -693,6 +696,9 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       // template parameter: no per-term predication)
       constexpr int NS = conv_ns(EPI);
       constexpr size_t NW = (size_t)1 << LOG_N;
+      u32 hc0[NS], hc1[NS];  // the constants' 31-bit digits (uniform, SGPRs)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) split31(ep.h[i], hc0[i], hc1[i]);
 #pragma unroll
       for (int c0 = 0; c0 < R; c0 += 4) {
         u64 sv[4][NS];
@@ -702,7 +708,9 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
           for (int i = 0; i < NS; ++i)
             sv[j][i] = ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[c0 + j] = dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);  // < 4q
+        for (int j = 0; j < 4; ++j)
+          x[c0 + j] = CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                 // < 2q
+                                : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);  // < 4q
       }
     } else {
       // the first forward pass may read out of place (NttArgs::src)

@@ -342,6 +342,15 @@ struct BehzDev {
   u64 h_b_q_R[BEHZ_MAXL][BEHZ_MAXL];  // (B/b_j) mod q_i
 };
 
+#ifndef BEHZ_COLS
+#define BEHZ_COLS 1  // BEHZ dot products as 31-bit column sums (dot_cols_canon); 0: dot_mont
+#endif
+template <int NL, bool SP>
+__device__ __forceinline__ u64 behz_dot(const u64 (&v)[NL], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
+  if constexpr (BEHZ_COLS) return dot_cols_canon<NL, SP>(v, h, hs, ns, m);
+  else return dot_mont<NL, SP>(v, h, hs, ns, m);
+}
+
 // behz_extend (oracle): fastbconv_m_tilde then sm_mrq.  x [L] coef -> [nB] coef
 // EX: L == NL exactly (nB = L + 1 always), so every loop is unrolled with no
 // per-limb guards (the C3 parameters); otherwise NL bounds L.
@@ -378,7 +387,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
     if (EX || j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
       // (sum_i v_i (Q/q_i) + r Q) 2^-32, the 2^-32 folded into the weights
-      const u64 xbj = dot_mont<NL, SP>(v, &bz->hx_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 xbj = behz_dot<NL, SP>(v, &bz->hx_R[0][j], BEHZ_MAXL + 1, L, m);
       const u64 rr = r >= 0x80000000u ? (u64)r + m.q - (1ull << 32) : (u64)r;   // centered r mod b
       d[j * N] = csub63(xbj + csub63(mont_mul<SP>(rr, bz->qx_R[j], m), m.q), m.q);
     }
@@ -419,7 +428,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   for (int j = 0; j < NL + 1; ++j) {
     if (EX || j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
-      const u64 cv = dot_mont<NL, SP>(v, &bz->hf_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 cv = behz_dot<NL, SP>(v, &bz->hf_R[0][j], BEHZ_MAXL + 1, L, m);
       const u64 tx = csub63(mont_mul<SP>(xb[j * N], bz->tf_R[j], m), m.q);
       const u64 wj = csub63(tx + cv, m.q);
       if (j == (int)nB - 1) flsk = wj;
@@ -429,13 +438,13 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
     }
   }
   const ModInfo msk = mods[bz->bsk0 + nB - 1];
-  const u64 alpha = sub_mod(dot_mont<NL, SP>(w, bz->hbm_R, 1, nB - 1, msk), flsk, msk.q);  // B^-1 folded in
+  const u64 alpha = sub_mod(behz_dot<NL, SP>(w, bz->hbm_R, 1, nB - 1, msk), flsk, msk.q);  // B^-1 folded in
   const bool neg = alpha > msk.q / 2;
   const u64 amag = neg ? msk.q - alpha : alpha;
   u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
   for (int i = 0; i < (EX ? NL : (int)L); ++i) {
     const ModInfo m = mods[i];
-    const u64 cq = dot_mont<NL, SP>(w, &bz->h_b_q_R[0][i], BEHZ_MAXL, nB - 1, m);
+    const u64 cq = behz_dot<NL, SP>(w, &bz->h_b_q_R[0][i], BEHZ_MAXL, nB - 1, m);
     const u64 ab = csub63(mont_mul<SP>(amag, bz->b_mod_q_R[i], m), m.q);
     const u64 r = csub63(cq + (neg ? ab : m.q - ab), m.q);  // cq -/+ ab (ab = 0 gives cq + q -> cq)
     o[i * N] = r;
