@@ -343,7 +343,7 @@ struct BehzDev {
 };
 
 #ifndef BEHZ_COLS
-#define BEHZ_COLS 1  // BEHZ dot products as 31-bit column sums (dot_cols_canon); 0: dot_mont
+#define BEHZ_COLS 0  // 1: BEHZ dot products as 31-bit column sums (dot_cols_canon): extend +8%, floor -0.7%, C3 -0.9% (profiles/r03/ab_conv_cols.txt)
 #endif
 template <int NL, bool SP>
 __device__ __forceinline__ u64 behz_dot(const u64 (&v)[NL], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
