@@ -199,6 +199,46 @@ HD u64 mont_mul_gen(u64 a, u64 b, const ModInfo &m) {
   return Y + (((u64)m1 * q0 + (u32)X) >> 32);
 }
 
+// M independent mont_mul_gen products phase by phase (as mont_mul_sp_vec), so
+// the dependent chains of different products interleave
+template <int M>
+HD void mont_mul_gen_vec(u64 (&r)[M], const u64 (&a)[M], const u64 (&b)[M], const ModInfo &m) {
+  const u32 q0 = (u32)m.q, q1 = (u32)(m.q >> 32), qi = (u32)m.qinv_neg;
+  u64 P[M], V[M];
+  u32 mk[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    P[i] = (u64)(u32)a[i] * (u32)b[i];
+    OPAQUE(P[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) mk[i] = (u32)P[i] * qi;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    V[i] = (u64)mk[i] * q1 + ((u64)(u32)(a[i] >> 32) * (u32)b[i] + (P[i] >> 32));
+    OPAQUE(V[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    V[i] += ((u64)mk[i] * q0 + (u32)P[i]) >> 32;
+    OPAQUE(V[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    P[i] = (u64)(u32)a[i] * (u32)(b[i] >> 32) + V[i];  // X
+    OPAQUE(P[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) mk[i] = (u32)P[i] * qi;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    V[i] = (u64)mk[i] * q1 + ((u64)(u32)(a[i] >> 32) * (u32)(b[i] >> 32) + (P[i] >> 32));
+    OPAQUE(V[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) r[i] = V[i] + (((u64)mk[i] * q0 + (u32)P[i]) >> 32);
+}
+
 template <bool SP>
 HD u64 mont_mul(u64 a, u64 b, const ModInfo &m) {  // a*b*2^-64, [0,2q); a < 2^63, b < q
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -51,6 +51,9 @@
 #ifndef KSP_PD
 #define KSP_PD 2  // PRO_KSP operand prefetch depth (elements)
 #endif
+#ifndef GEN_VEC
+#define GEN_VEC 0  // 1: generic moduli's butterfly and KS products in lock-step (mont_mul_gen_vec): -0.6% on OpenFHE-style primes, profiles/r03/ab_gen_vec.txt
+#endif
 #ifndef CONV_COLS
 #define CONV_COLS 1  // PRO_CONV: 31-bit column sums (dot_cols); 0: dot_mont_lazy
 #endif
@@ -271,7 +274,7 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
   for (int ti = 0; ti < GP::nb; ++ti) {
     const int tau = INV ? GP::nb - 1 - ti : ti;
     const int half = 1 << (GP::nb - 1 - tau);
-    if constexpr (SP) {
+    if constexpr (SP || GEN_VEC) {
       // the R/2 butterflies of this stage in lock-step (see mont_mul_sp_vec)
       constexpr int H = R / 2;
       u64 A[H], Wt[H], V[H], U[H];
@@ -306,7 +309,8 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
           A[i] = (X + q2p1) + ~Y;
         }
       }
-      mont_mul_sp_vec<H>(V, A, Wt, mi.q_hi);
+      if constexpr (SP) mont_mul_sp_vec<H>(V, A, Wt, mi.q_hi);
+      else mont_mul_gen_vec<H>(V, A, Wt, mi);
 #pragma unroll
       for (int i = 0; i < H; ++i) {
         if (!INV) {
@@ -497,6 +501,8 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
             }
             if constexpr (SP) {
               mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+            } else if constexpr (GEN_VEC) {
+              mont_mul_gen_vec<KD>(pr, e, k, mi);
             } else {
 #pragma unroll
               for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
@@ -663,6 +669,8 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         }
         if constexpr (SP) {
           mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+        } else if constexpr (GEN_VEC) {
+          mont_mul_gen_vec<KD>(pr, e, k, mi);
         } else {
 #pragma unroll
           for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
