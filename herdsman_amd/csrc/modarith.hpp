@@ -369,6 +369,38 @@ HD u64 dot_cols(const u64 (&v)[NS], const u32 (&h0)[NS], const u32 (&h1)[NS], co
   const u64 hi = (c1 >> 33) + (c2 >> 2) + (lo1 < c0) + (lo < lo1);
   return mont_reduce<SP>(U128{lo, hi}, m);
 }
+// The same sum for a special modulus m = mh 2^32 + 1 < 2^60 (h1 < 2^29): the
+// reduction runs on the columns themselves, as Montgomery rounds of 31, 31
+// and 2 bits (m = 1 mod 2^31, so each quotient digit is -t mod 2^k and its
+// multiple of m is u (m >> k) 2^k + u): C0 is folded into C1's accumulator, C1
+// into C2's, with no 128-bit combine.  Each accumulator starts at 2^k - 1, so
+// its top (acc >> k) already carries the round's "+ [t != 0]" and the digit is
+// ~acc mod 2^k.  Bounds: C1 < 2^63 + 2^62 + 2^61, C2 < 2^62; result < 2q.
+template <int NS>
+HD u64 dot_cols_sp60(const u64 (&v)[NS], const u32 (&h0)[NS], const u32 (&h1)[NS], u32 q_hi) {
+  static_assert(NS >= 1 && NS <= 4, "column sums stay below 2^64 for at most 4 terms");
+  u32 v0[NS], v1[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) v0[i] = (u32)v[i] & 0x7FFFFFFFu, v1[i] = (u32)(v[i] >> 31);
+  const u32 mh2 = q_hi << 1;  // m >> 31
+  u64 c = 0x7FFFFFFFull;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) c += (u64)v0[i] * h0[i];
+  u32 u = ~(u32)c & 0x7FFFFFFFu;
+  c = (u64)u * mh2 + ((c >> 31) + 0x7FFFFFFFull);
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    c += (u64)v0[i] * h1[i];
+    c += (u64)v1[i] * h0[i];
+  }
+  u = ~(u32)c & 0x7FFFFFFFu;
+  c = (u64)u * mh2 + ((c >> 31) + 3);
+#pragma unroll
+  for (int i = 0; i < NS; ++i) c += (u64)v1[i] * h1[i];
+  const u32 u2 = ~(u32)c & 3u;
+  return (u64)(u2 << 30) * q_hi + (c >> 2);  // m >> 2 = q_hi 2^30
+}
+
 HD void split31(u64 h, u32 &h0, u32 &h1) {
   h0 = (u32)h & 0x7FFFFFFFu;
   h1 = (u32)(h >> 31);

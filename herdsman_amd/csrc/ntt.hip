@@ -54,6 +54,9 @@
 #ifndef GEN_VEC
 #define GEN_VEC 0  // 1: generic moduli's butterfly and KS products in lock-step (mont_mul_gen_vec): -0.6% on OpenFHE-style primes, profiles/r03/ab_gen_vec.txt
 #endif
+#ifndef CONV_SP60
+#define CONV_SP60 1  // PRO_CONV on special targets below 2^60: the column sums reduced in place (dot_cols_sp60); headline +0.8%, profiles/r03/ab_conv_sp60.txt
+#endif
 #ifndef CONV_COLS
 #define CONV_COLS 1  // PRO_CONV: 31-bit column sums (dot_cols); 0: dot_mont_lazy
 #endif
@@ -717,8 +720,9 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
             sv[j][i] = ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          x[c0 + j] = CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                 // < 2q
-                                : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);  // < 4q
+          x[c0 + j] = CONV_COLS && SP && WIDE && CONV_SP60 ? dot_cols_sp60<NS>(sv[j], hc0, hc1, mi.q_hi)  // < 2q
+                      : CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                                  // < 2q
+                                  : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);                   // < 4q
       }
     } else {
       // the first forward pass may read out of place (NttArgs::src)
