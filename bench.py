@@ -195,9 +195,11 @@ def main():
         lanes.append((c_i, s_i))
 
     # ---- relinearisation key: rank 0 makes it, one RCCL broadcast to the others
+    # (seeded like the committed metric digest case, so that every rank can
+    # check its own outputs against that digest with the key it RECEIVED)
     rlk = hb.empty(ctx.key_shape(), device=dev)
     if rank == 0:
-        ctx.fill_uniform(rlk, seed=0x524C4B)
+        ctx.fill_uniform(rlk, seed=SELF_CHECK["seed_key"])
     torch.cuda.synchronize(dev)
     bcast, bcast_err, key_ok = "none (1 rank)", None, True
     if world > 1:
@@ -258,6 +260,14 @@ def main():
     else:
         per_rank = [(my * steps / mine) if mine > 0 else 0.0]
     value = G * steps / elapsed if steps else 0.0
+
+    # ---- per-rank output check: every lane context of every rank recomputes the
+    # committed metric digest case with the broadcast key (after the timed region)
+    mine_ok = rank_self_check(hb, lanes, rlk, dev)
+    per_rank_ok = [mine_ok]
+    if world > 1:
+        per_rank_ok = [None] * world
+        dist.all_gather_object(per_rank_ok, mine_ok)
 
     # ---- dominant kernel group: forward NTT over the ModUp-sized wave (36 limbs per ct)
     limbs = B * 3 * L
@@ -329,6 +339,9 @@ def main():
             "key_bcast_via": bcast,
             "key_bcast_error": bcast_err,
             "key_identical_on_all_ranks": key_ok,
+            "per_rank_bitexact": [bool(v["ok"]) for v in per_rank_ok],
+            "per_rank_check": {"case": SELF_CHECK["case"], "lanes": [v["lanes"] for v in per_rank_ok],
+                               "source": "tests/golden/digests.json (CPU oracle, make_digests.py)"},
             "algorithmic_GBps_ct_mult": round(value / n_gpus * 6 * L * n * 8 / 1e9, 1),
             "cpu_baseline": cpu,
             "secondary": secondary,
@@ -336,7 +349,48 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not all(v["ok"] for v in per_rank_ok):
+        if rank == 0:
+            print(f"bench.py: output digest mismatch on rank(s) "
+                  f"{[r for r, v in enumerate(per_rank_ok) if not v['ok']]}", file=sys.stderr, flush=True)
+        return 4
     return 0
+
+
+def _load_self_check():
+    """The metric digest case of tests/golden (committed SHA-256 of the CPU
+    oracle's output on SplitMix64 inputs with fixed seeds)."""
+    case = "metric_ckks_mul_relin_n65536_l12"
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))[case]
+    # the seeds of tests/golden/full_size_cases.py (SEED_A, SEED_B, SEED_KEY)
+    return {"case": case, "sha256": d["sha256"], "moduli": d["moduli"],
+            "seed_a": 0x48455244, "seed_b": 0x48455245, "seed_key": 0x4B4559}
+
+
+SELF_CHECK = _load_self_check()
+
+
+def rank_self_check(hb, lanes, rlk, dev):
+    """{"ok", "lanes"}: each lane context's product of the digest case's inputs
+    (generated on the device) with this rank's copy of the key hashes to the
+    committed digest.  A wrong-but-fast rank, a lane whose context diverged or a
+    corrupted key broadcast fails the run (exit 4)."""
+    import hashlib
+
+    import torch
+    n = 1 << LOG_N
+    res = []
+    for c, s in lanes:
+        if [int(q) for q in c.moduli] != SELF_CHECK["moduli"]:
+            res.append(False)
+            continue
+        a = c.fill_uniform(hb.empty((1, 2, L, n), device=dev), seed=SELF_CHECK["seed_a"])
+        b = c.fill_uniform(hb.empty((1, 2, L, n), device=dev), seed=SELF_CHECK["seed_b"])
+        y = hb.empty((1, 2, L, n), device=dev)
+        c.mul_relin(a, b, rlk, y)
+        torch.cuda.synchronize(dev)
+        res.append(hashlib.sha256(hb.to_host(y).tobytes()).hexdigest() == SELF_CHECK["sha256"])
+    return {"ok": bool(res) and all(res), "lanes": res}
 
 
 def wave_plan(G, batch, streams, pool, world, rank, stagger=True):

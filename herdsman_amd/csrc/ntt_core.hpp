@@ -1,0 +1,1115 @@
+// ntt_core.hpp -- negacyclic NTT / INTT pass kernels for gfx950 (templates; host entry points in ntt*.hip).
+//
+// Algorithm (same transform as the oracle's orc_ntt_fwd, oracle/fhe_oracle.c):
+// Harvey's lazy Cooley-Tukey forward (natural in, bit-reversed out, values in
+// [0,4q) between stages, or [0,8q) with fewer reductions for q < 2^60 -- see
+// wide_csub) and Gentleman-Sande inverse ([0,2q)).  The twiddle of
+// butterfly (j, j+t) at global stage s is psi^brv(2^s + (j >> (logN - s))),
+// stored in Montgomery form (psi^e * 2^64 mod q) so one mont_mul = 6
+// quarter-rate multiplies gives the exact product (modarith.hpp).
+//
+// MI355X mapping.  One limb-polynomial of N u64 words is split into passes;
+// a pass owns global stages [s0, s0+S) and works on independent
+// sub-transforms of 2^S elements at stride N >> (s0+S):
+//   N <= 2^13 : ONE pass, one residue per workgroup (up to 64 KiB of LDS) --
+//               the north-star "one-residue-per-WG"; at N = 2^14 (128 KiB, one
+//               1024-thread workgroup per CU) the fused prologue/epilogue
+//               passes keep it, while plain NTTs run two 7-stage passes with 4
+//               workgroups per CU, which measured 2% faster (C2) despite the
+//               intermediate's round trip;
+//   N  = 2^15..2^17 : two passes (column pass of stride N/2^S1, then row pass
+//               of contiguous 2^S2 blocks), because a 512 KiB N=2^16 residue
+//               exceeds the 160 KiB LDS of a CU.
+// Pass geometry (N, stages, stride, last) is compile-time, so every element
+// address is one per-thread 32-bit offset plus a constant on a scalar base.
+// Inside a pass each thread keeps R = 16 elements in VGPRs and runs LOGR = 4
+// butterfly stages in registers per "group"; groups are separated by ONE LDS
+// exchange (write, barrier, read).  The first group loads straight from HBM
+// and the last group stores straight to HBM (128 B row segments for column
+// passes, 16 contiguous words per lane for row passes), and each group's
+// twiddles are fetched while the previous group computes, so neither the
+// data nor the twiddle latency sits on the VALU critical path.
+#pragma once
+#include <algorithm>
+
+#include "context.hpp"
+
+#ifndef KSQ_PD
+#define KSQ_PD 2  // EPI_KSQ operand prefetch depth (elements; 3 measured no faster, profiles/r03/ab_ksq_pd_aut.txt)
+#endif
+#ifndef TENSOR_CHUNK
+#define TENSOR_CHUNK 65535u  // ciphertexts per INTT(d2) pass pair (MALL-sized chunks: see DESIGN §4)
+#endif
+#ifndef COMBINE_CHUNK
+#define COMBINE_CHUNK 65534u  // polys per NTT(conv) pass pair (even)
+#endif
+#ifndef KSQ_GI
+#define KSQ_GI 1  // EPI_KSQ: (limb, row block) groups interleaved per XCD (4: kernel -1.6% but headline -0.2%, profiles/r03/ab_group_interleave.txt)
+#endif
+#ifndef KSP_GI
+#define KSP_GI 1  // PRO_KSP: the same
+#endif
+#ifndef KSP_PD
+#define KSP_PD 2  // PRO_KSP operand prefetch depth (elements)
+#endif
+#ifndef GEN_VEC
+#define GEN_VEC 0  // 1: generic moduli's butterfly and KS products in lock-step (mont_mul_gen_vec): -0.6% on OpenFHE-style primes, profiles/r03/ab_gen_vec.txt
+#endif
+#ifndef CONV_SP60
+#define CONV_SP60 1  // PRO_CONV on special targets below 2^60: the column sums reduced in place (dot_cols_sp60); headline +0.8%, profiles/r03/ab_conv_sp60.txt
+#endif
+#ifndef CONV_COLS
+#define CONV_COLS 1  // PRO_CONV: 31-bit column sums (dot_cols); 0: dot_mont_lazy
+#endif
+#ifndef AUT_PD
+#define AUT_PD 2  // PRO_AUTOMORPH gather prefetch depth (elements)
+#endif
+#ifndef CONV_T
+#define CONV_T 1  // PRO_CONV target limbs per workgroup (conv_multi_body); 2 as first written spilled 34-98 VGPRs: headline 15.8k against 18.2k
+#endif
+#ifndef CONV_PIPE
+#define CONV_PIPE 1  // conv_multi_body: scheduling barriers between the prologue's source chunks
+#endif
+#ifndef MODUP_COL_SPLIT
+#define MODUP_COL_SPLIT 1
+#endif
+
+struct NttArgs {
+  LimbMap map;
+  const u64 *tw;         // [nmod][N], Montgomery form
+  const ModInfo *mods;   // [nmod]
+  const u64 *ninv;       // [nmod], N^-1 in Montgomery form
+  u32 log_n;
+  // inverse only: leave out the N^-1 scaling (the consumer's conversion
+  // constants carry it, fhe_ctx::fold_ninv); outputs stay canonical
+  u32 noscale;
+  // inverse only: if set, the last pass multiplies by scale[mod] (Montgomery
+  // form) instead of N^-1: the per-source constant of a following base
+  // conversion rides on the transform (fhe_ctx::d_iscale), so its outputs are
+  // already the conversion's canonical v_i = [x (S/s_i)^-1]_{s_i}
+  const u64 *scale;
+  // forward only: the first pass reads its limbs from src (the same layout as
+  // map.base: poly stride and limb positions) instead of transforming in
+  // place -- an out-of-place NTT, so a caller's input is never copied first
+  const u64 *src;
+  // forward only: leave the outputs in the lazy range (below 8q < 2^63), for a
+  // consumer whose Montgomery products accept any input below 2^63 (the KS
+  // inner product on special moduli)
+  u32 lazy_out;
+  // EPI_COMBINE (forward last pass over the ModDown conversion conv [p][L][N],
+  // p = 2 ct + b): out[p][i] = (add_mask bit b ? base[p][i] : 0) + (acc[p][i] - conv) P^-1
+  const u64 *e_acc;      // [p][e_acc_stride][N]
+  const u64 *e_base;     // [p][L][N], may alias e_out
+  u64 *e_out;            // [p][L][N]
+  const u64 *e_pinv;     // [L] P^-1 R mod q_i
+  u32 e_acc_stride;
+  u32 e_add_mask;
+  u32 e_g;  // combine: 0, or the base is read as sigma_g(base) (rotation: sigma_g(c0) never stored)
+  // EPI_KSQ (EPI_COMBINE whose acc_Q is the key-switching inner product, formed
+  // here instead of being read): acc[p][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1,
+  // p = 2 ct + b, with ext [ct][e_ndig][e_QP][N] and ksk [e_ndig][2][e_QP][N]
+  const u64 *e_ext, *e_ksk;
+  u32 e_ndig, e_QP;
+  // PRO_TENSOR (first pass of the inverse NTT of d2 in CKKS mul+relin, poly =
+  // ciphertext): the pass reads the operands a, b [ct][2][L][N] instead of d2,
+  // writes the relinearisation base out[ct][0] = a0 b0, out[ct][1] = a0 b1 + a1 b0
+  // and the own-digit ext slot d2 R, and transforms d2 = a1 b1 (the tensor
+  // product fused here: d2 never makes an HBM round trip before the INTT)
+  const u64 *t_a, *t_b;
+  u64 *t_out;            // may alias t_a / t_b (element-wise)
+  u64 *t_ext;            // [ct][ndig][QP][N]
+  u32 t_L, t_QP, t_alpha, t_ndig;
+  // PRO_AUTOMORPH (first pass of the inverse NTT of sigma_g(c1) in CKKS
+  // rotation): reads the input ciphertext t_a [ct][2][L][N] (NTT form) at the
+  // permuted slots, writes the key-switch base t_out[ct][0] = sigma_g(c0) and
+  // the own-digit ext slot sigma_g(c1) R, and transforms sigma_g(c1)
+  u32 t_g;
+  // PRO_CONV (first (column) pass of a forward NTT): the pass's input limb is
+  // the fast base conversion y_m = sum_i v_i h[i][m] of c_ns canonical source
+  // limbs v_i at c_src[poly][c_src_first + i] (poly stride c_src_stride limbs),
+  // m = the active-limb index of the map; conv never makes an HBM round trip
+  const u64 *c_src;
+  const u64 *c_h;        // [ns][nd] ConvTab.h
+  u32 c_src_stride, c_src_first, c_ns, c_nd;
+};
+
+// The passes shared by several entry points, compiled once (ntt.hip, ntt_conv*.hip):
+// plain forward / inverse passes (single = N <= 2^14 one-pass, col, row) and
+// the forward column pass with the conversion prologue over a.c_ns sources.
+int ntt_single_plain(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs);
+int ntt_col_plain(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs);
+int ntt_row_plain(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs);
+int ntt_conv_col(fhe_ctx *c, const NttArgs &a, u32 n_jobs);
+int ntt_conv_col12(fhe_ctx *c, const NttArgs &a, u32 n_jobs);
+
+namespace {
+
+
+
+// EPI_COMBINE: epilogue of a forward last pass; PRO_TENSOR: prologue of an
+// inverse first (row) pass
+// PRO_BFVT: prologue of the inverse first (row) pass of the BFV tensor
+// product e = (a0 b0, a0 b1 + a1 b0, a1 b1) in one RNS base
+// PRO_CONV: prologue of a forward first (column) pass, the base conversion
+// that produces its input
+// EPI_KSQ + d - 1: EPI_COMBINE with the Q limbs' key-switching inner product
+// over d = 1..4 digits fused in (the digit count is compile-time)
+// PRO_CONV + ns - 1: the conversion prologue over ns = 1..4 source limbs (compile-time)
+// PRO_KSP + d - 1: prologue of the inverse first (row) pass of INTT(acc_P):
+// the P limbs' key-switching inner product over d = 1..4 digits (acc_P is
+// formed at the load positions and never stored)
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, EPI_KSQ = 6, PRO_CONV = 11,
+       PRO_KSP = 16 };
+__host__ __device__ constexpr bool is_conv(int e) { return e >= PRO_CONV && e < PRO_CONV + 4; }
+__host__ __device__ constexpr int conv_ns(int e) { return e - PRO_CONV + 1; }
+__host__ __device__ constexpr bool is_ksq(int e) { return e >= EPI_KSQ && e < EPI_KSQ + 4; }
+__host__ __device__ constexpr int ksq_digits(int e) { return e - EPI_KSQ + 1; }
+__host__ __device__ constexpr bool is_combine(int e) { return e == EPI_COMBINE || is_ksq(e); }
+__host__ __device__ constexpr bool is_ksp(int e) { return e >= PRO_KSP && e < PRO_KSP + 4; }
+__host__ __device__ constexpr int ksp_digits(int e) { return e - PRO_KSP + 1; }
+
+// NTT-domain automorphism: slot k holds a(psi^e), e = 2 brv(k) + 1, and
+// sigma_g(a)(psi^e) = a(psi^(e g)); the byte offset of the source slot of k.
+// The 64 lanes of a coalesced load read one aligned 64-slot block of the
+// source (g only permutes inside it).
+template <int LOG_N>
+__device__ __forceinline__ u32 aut_src(u32 k, u32 g) {
+  constexpr u32 MASK = (2u << LOG_N) - 1;
+  const u32 e = (((__brev(k) >> (32 - LOG_N)) << 1) | 1) * g & MASK;
+  return (__brev(e >> 1) >> (32 - LOG_N)) << 3;
+}
+
+// per-workgroup epilogue / prologue operands (resolved once per limb)
+struct EpiRow {
+  const u64 *acc;
+  const u64 *kext, *kksk;  // EPI_KSQ, PRO_KSP: digit 0's ext / key row of this limb (digit j at + j stride)
+  size_t ext_j, ksk_j;     // digit strides (words)
+  const u64 *base;
+  u64 *out;
+  u64 pinv;
+  bool add;
+  const u64 *a0, *a1, *b0, *b1;  // PRO_TENSOR
+  u64 *o0, *o1, *ext;
+  u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base or null; ext); combine: e_g
+  u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is
+  const u64 *src;  // PRO_CONV: source limb 0 of this poly (limb i at src + i N)
+  u64 h[4];        // PRO_CONV: h[i][m] of this workgroup's target limb
+};
+
+// LDS slot of element k of sub-transform w: one pad word per 16 words and per
+// sub-transform keeps every exchange pattern free of bank conflicts
+// (SQ_LDS_BANK_CONFLICT = 0), and the slot stays affine in the register index
+// r, so the 16 accesses of a thread share one address register.
+// Element access at a 32-bit word index from a scalar (per-workgroup) base:
+// the byte offset is formed in 32 bits so the load/store uses the
+// `global_load v, v_off, s[base:base+1]` form (one VALU op per address).
+__device__ __forceinline__ u64 ld_at(const u64 *base, u32 idx) {
+  return *(const u64 *)((const char *)base + (idx << 3));
+}
+// the same at a byte offset (per-thread offsets computed once per pass)
+__device__ __forceinline__ u64 ld_b(const u64 *base, u32 off) { return *(const u64 *)((const char *)base + off); }
+// a pass's own data words are read once: non-temporal (A/B on one box: the
+// forward NTT -1%; the fused prologue/epilogue operand streams lose with nt,
+// so they keep ld_b; nt stores measured neutral)
+__device__ __forceinline__ u64 ld_d(const u64 *base, u32 off) {
+  return __builtin_nontemporal_load((const u64 *)((const char *)base + off));
+}
+__device__ __forceinline__ void st_b(u64 *base, u32 off, u64 v) { *(u64 *)((char *)base + off) = v; }
+
+template <int S>
+__device__ __forceinline__ u32 lds_idx(u32 w, u32 k) {
+  constexpr u32 SUB = 1u << S;
+  constexpr u32 PAD = SUB + (SUB >> 4) + 1;
+  return w * PAD + k + (k >> 4);
+}
+template <int S, int W>
+constexpr size_t lds_bytes() {
+  return (size_t)W * ((1u << S) + (1u << S >> 4) + 1) * sizeof(u64);
+}
+
+
+// Group geometry (compile time): group g covers local stages
+// [g*LOGR, g*LOGR + nb); its butterfly bits are k bits [p, p+nb).  A thread
+// holds R = 2^LOGR elements k(r) = hh<<(p+nb+ex) | rx<<(p+nb) | rb<<p | lo_t;
+// k_thr(ts) is the per-thread part, k_reg(r) the compile-time part.
+template <int S, int LOGR, int G>
+struct Grp {
+  static constexpr int nb = (S - G * LOGR) < LOGR ? (S - G * LOGR) : LOGR;
+  static constexpr int ex = LOGR - nb;
+  static constexpr int p = S - G * LOGR - nb;
+  static constexpr int NTW = (1 << ex) * ((1 << nb) - 1);  // distinct twiddles per thread
+  __device__ static __forceinline__ u32 k_thr(u32 ts) {
+    return ((ts >> p) << (p + nb + ex)) | (ts & ((1u << p) - 1));
+  }
+  static constexpr u32 k_reg(int r) {
+    return ((u32)(r >> nb) << (p + nb)) | ((u32)(r & ((1 << nb) - 1)) << p);
+  }
+  __device__ static __forceinline__ u32 k_of(int r, u32 ts) { return k_thr(ts) | k_reg(r); }
+  // slot of (tau, rx, d) in the per-thread twiddle array, d < 2^tau
+  __device__ static constexpr int slot(int tau, int rx, int d) { return rx * ((1 << nb) - 1) + (1 << tau) - 1 + d; }
+  // twiddle of local stage sigma = G*LOGR + tau: index 2^(s0+sigma) + hi 2^sigma + kk,
+  // kk = (hh 2^ex + rx) 2^tau + d.  The thread-dependent part (hi, hh) is one
+  // 32-bit offset per tau; the rest is a compile-time offset on a scalar base.
+  template <int S0>
+  __device__ static __forceinline__ void load_tw(u64 (&t)[16], const u64 *tw, u32 hi, u32 ts) {
+    const u32 hh = ts >> p;
+#pragma unroll
+    for (int tau = 0; tau < nb; ++tau) {
+      const int sigma = G * LOGR + tau;
+      const u32 thr = (hi << sigma) + (hh << (ex + tau));
+#pragma unroll
+      for (int rx = 0; rx < (1 << ex); ++rx)
+#pragma unroll
+        for (int d = 0; d < (1 << tau); ++d)
+          t[slot(tau, rx, d)] = ld_at(tw + ((1u << (S0 + sigma)) + ((u32)rx << tau) + (u32)d), thr);
+    }
+  }
+};
+
+// x - m if that is non-negative, else x (x, m < 2^63; neg_m = -m), selected
+// by the sign word with two v_bfi_b32: no VCC compare/select, so no hazard nops
+__device__ __forceinline__ u64 harvey_csub(u64 x, u64 neg_m) {
+  const u64 d = x + neg_m;
+  const u32 m = (u32)((int32_t)(u32)(d >> 32) >> 31);  // all ones iff d < 0
+  const u64 mm = ((u64)m << 32) | m;
+  return (x & mm) | (d & ~mm);
+}
+
+// Forward lazy-range schedule.  NARROW (every modulus): values in [0,4q)
+// between stages, U = csub(X, 2q) at every stage (Harvey).  WIDE (moduli
+// q < 2^60, i.e. 8q < 2^63, the Montgomery input bound; the special product
+// is below 1.5q, the generic one below 2q): a stage with
+// input bound B q gives outputs below (B+2) q without any reduction
+// (X' = X + V < (B+1.5) q, Y' = X + 2q - V < (B+2) q), so from an input in
+// [0,4q) the stages run 4 -> 6 -> 8 and then alternate csub(X, 4q) (8 -> 6)
+// with none (6 -> 8): global stages 2, 4, 6, ... reduce, the others do not,
+// and 7 of the 16 stages of N = 2^16 reduce instead of 16.  Pass outputs stay
+// below 8q < 2^63; the last stage canonicalises from [0,8q).
+__host__ __device__ constexpr bool wide_csub(int gs) { return gs >= 2 && (gs & 1) == 0; }
+
+template <int S, int LOGR, int G, int S0, bool INV, bool SP, bool WIDE>
+__device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 q2, const ModInfo &mi) {
+  using GP = Grp<S, LOGR, G>;
+  constexpr int R = 1 << LOGR;
+#pragma unroll
+  for (int ti = 0; ti < GP::nb; ++ti) {
+    const int tau = INV ? GP::nb - 1 - ti : ti;
+    const int half = 1 << (GP::nb - 1 - tau);
+    if constexpr (SP || GEN_VEC) {
+      // the R/2 butterflies of this stage in lock-step (see mont_mul_sp_vec)
+      constexpr int H = R / 2;
+      u64 A[H], Wt[H], V[H], U[H];
+      int lo_idx[H];
+      {
+        int n = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int rb = r & ((1 << GP::nb) - 1), rx = r >> GP::nb;
+          if (rb & half) continue;
+          lo_idx[n] = r;
+          Wt[n] = t[GP::slot(tau, rx, rb >> (GP::nb - tau))];
+          ++n;
+        }
+      }
+      // 64-bit adds of SGPR constants as single v_lshl_add_u64 (no carry
+      // chain through VCC, which costs s_nop wait states): a - b = a + (2q+1) + ~b - 2q
+      u64 nq2 = 0 - q2, q2p1 = q2 + 1, nq4 = 0 - 2 * q2;
+      asm("" : "+s"(nq2));
+      asm("" : "+s"(q2p1));
+      asm("" : "+s"(nq4));
+      const int gs = S0 + G * LOGR + tau;  // global stage
+      const bool red = !WIDE || wide_csub(gs);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        const u64 X = x[lo_idx[i]], Y = x[lo_idx[i] + half];
+        if (!INV) {
+          U[i] = !red ? X : harvey_csub(X, WIDE ? nq4 : nq2);
+          A[i] = Y;
+        } else {
+          U[i] = harvey_csub(X + Y, nq2);
+          A[i] = (X + q2p1) + ~Y;
+        }
+      }
+      if constexpr (SP) mont_mul_sp_vec<H>(V, A, Wt, mi.q_hi);
+      else mont_mul_gen_vec<H>(V, A, Wt, mi);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        if (!INV) {
+          x[lo_idx[i]] = U[i] + V[i];
+          x[lo_idx[i] + half] = (U[i] + q2p1) + ~V[i];
+        } else {
+          x[lo_idx[i]] = U[i];
+          x[lo_idx[i] + half] = V[i];
+        }
+      }
+      continue;
+    }
+    // generic moduli: the same lazy schedules (the generic Montgomery product
+    // is below 2q and accepts any input below 8q, since 8q^2 < q 2^64)
+    u64 nq2 = 0 - q2, q2p1 = q2 + 1, nq4 = 0 - 2 * q2;
+    asm("" : "+s"(nq2));
+    asm("" : "+s"(q2p1));
+    asm("" : "+s"(nq4));
+    const bool red = !WIDE || wide_csub(S0 + G * LOGR + tau);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int rb = r & ((1 << GP::nb) - 1), rx = r >> GP::nb;
+      if (rb & half) continue;
+      const u64 w = t[GP::slot(tau, rx, rb >> (GP::nb - tau))];
+      u64 &X = x[r];
+      u64 &Y = x[r + half];
+      if (!INV) {
+        const u64 uu = !red ? X : harvey_csub(X, WIDE ? nq4 : nq2);
+        const u64 v = mont_mul<SP>(Y, w, mi);
+        X = uu + v;
+        Y = (uu + q2p1) + ~v;
+      } else {
+        const u64 uu = X, vv = Y;
+        X = harvey_csub(uu + vv, nq2);
+        Y = mont_mul<SP>((uu + q2p1) + ~vv, w, mi);
+      }
+    }
+  }
+}
+
+// Compile-time pass geometry.  A pass owns global stages [S0, S0+S) of an
+// N = 2^LOG_N transform; column passes work at element stride 2^LS, row passes
+// on contiguous blocks.  The last pass canonicalises (and scales by N^-1).
+template <int LOG_N, int S, bool COLS, bool INV>
+struct PassGeo {
+  static constexpr bool single = S == LOG_N;
+  static constexpr int S0 = COLS ? 0 : LOG_N - S;
+  static constexpr int LS = COLS ? LOG_N - S : 0;
+  static constexpr bool LAST = single || (COLS == INV);
+};
+
+template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, bool WIDE, int EPI, int GI>
+__device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds, const u64 *tw, u64 *data,
+                                           u32 voff, u32 w, u32 ts, u32 hi, const NttArgs &a,
+                                           const ModInfo &mi, u32 mod, const EpiRow &ep) {
+  using PG = PassGeo<LOG_N, S, COLS, INV>;
+  constexpr int NG = (S + LOGR - 1) / LOGR;
+  constexpr int R = 1 << LOGR;
+  constexpr int G = INV ? NG - 1 - GI : GI;
+  using GP = Grp<S, LOGR, G>;
+  const u64 q = mi.q, q2 = 2 * q;
+  if constexpr (GI + 1 < NG) {
+    constexpr int GN = INV ? NG - 2 - GI : GI + 1;
+    u64 tn[16];
+    Grp<S, LOGR, GN>::template load_tw<PG::S0>(tn, tw, hi, ts);  // in flight while this group computes
+    run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
+    const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + (GP::k_reg(r) >> 4)] = x[r];
+    __syncthreads();
+    const u32 lr = lds_idx<S>(w, Grp<S, LOGR, GN>::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u32 kr = Grp<S, LOGR, GN>::k_reg(r);
+      x[r] = lds[lr + kr + (kr >> 4)];
+    }
+    group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, GI + 1>(x, tn, lds, tw, data, voff, w, ts, hi, a, mi,
+                                                                     mod, ep);
+  } else {
+    // EPI_COMBINE: the epilogue's acc and base words are in flight while the
+    // last group computes (the LDS footprint caps occupancy at 4 waves per
+    // SIMD, so the 128-VGPR budget has room for them)
+    constexpr int RE = is_combine(EPI) ? R : 1;
+    u64 pa[RE], pb[RE];
+    if constexpr (is_combine(EPI)) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (EPI == EPI_COMBINE) pa[r] = ld_b(ep.acc + Grp<S, LOGR, 0>::k_reg(r), voff);
+        const u32 kr = Grp<S, LOGR, 0>::k_reg(r);
+        if (!ep.add) pb[r] = 0;
+        else if (ep.g) pb[r] = ld_b(ep.base, aut_src<LOG_N>((voff >> 3) + kr, ep.g));  // sigma_g(base)
+        else pb[r] = ld_b(ep.base + kr, voff);
+      }
+    }
+    run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
+    // negated reduction constants pinned in SGPRs, so each conditional
+    // subtraction is one v_lshl_add_u64 with a scalar operand (left to itself
+    // the compiler forms x - m as a v_subrev_co/v_subb_co borrow chain with
+    // s_nop hazard padding)
+    u64 nq1 = 0 - q, nq2 = 0 - q2, nq4 = 0 - 2 * q2;
+    asm("" : "+s"(nq1));
+    asm("" : "+s"(nq2));
+    asm("" : "+s"(nq4));
+    // EPI_COMBINE: B q + 1, so (acc + cb1) + ~v = acc + B q - v
+    u64 cb1 = (WIDE ? 2 * q2 : q2) + 1;
+    asm("" : "+s"(cb1));
+    if constexpr (PG::LAST) {
+      if constexpr (is_combine(EPI)) {
+        // the ModDown finish takes NTT(conv) below 4q (WIDE) / 2q: one
+        // conditional subtraction instead of canonicalising (see the epilogue)
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = harvey_csub(x[r], WIDE ? nq4 : nq2);
+      } else if constexpr (!INV) {
+        if (!a.lazy_out) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            u64 v = x[r];
+            if (WIDE) v = harvey_csub(v, nq4);
+            x[r] = harvey_csub(harvey_csub(v, nq2), nq1);
+          }
+        }
+      } else {
+        if (a.noscale && !a.scale) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) x[r] = harvey_csub(x[r], nq1);  // GS outputs are below 2q
+        } else {
+          const u64 sc = a.scale ? a.scale[mod] : a.ninv[mod];
+#pragma unroll
+          for (int r = 0; r < R; ++r) x[r] = harvey_csub(mont_mul<SP>(x[r], sc, mi), nq1);
+        }
+      }
+    }
+    if constexpr (!COLS && G != 0) {
+      // EPI_KSQ: the key-switching operands (ext and key words, KD of each per
+      // element) are software-pipelined PD elements deep, and the first PD
+      // elements' loads are in flight across the re-layout barrier
+      constexpr int KD = is_ksq(EPI) ? ksq_digits(EPI) : 1;
+      constexpr int PD = is_ksq(EPI) && SP ? KSQ_PD : 1;
+      u64 ek[PD + 1][2 * KD];
+      if constexpr (is_ksq(EPI)) {
+#pragma unroll
+        for (int r = 0; r < PD; ++r) {
+          const u32 kr = Grp<S, LOGR, 0>::k_reg(r);
+#pragma unroll
+          for (int j = 0; j < KD; ++j) {
+            ek[r][j] = ld_b(ep.kext + j * ep.ext_j + kr, voff);
+            ek[r][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
+          }
+        }
+      }
+      // row pass ending in a group whose lanes each own contiguous words:
+      // re-layout through LDS so the HBM store is coalesced (group-0 layout)
+      const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + (GP::k_reg(r) >> 4)] = x[r];
+      __syncthreads();
+      using G0 = Grp<S, LOGR, 0>;
+      const u32 lr = lds_idx<S>(w, G0::k_thr(ts));
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32 kr = G0::k_reg(r);
+        const u64 v = lds[lr + kr + (kr >> 4)];
+        if constexpr (is_combine(EPI)) {
+          // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM.
+          // acc - conv is formed as acc + Bq - v (v < Bq, B = 4 WIDE / 2): below
+          // 5q < 2^63 for q < 2^60 and 3q < 2^63 for q < 2^61, inside the
+          // Montgomery input bound, whose product below 1.5q (2q generic)
+          // is canonicalised by one conditional subtraction
+          u64 acc;
+          if constexpr (is_ksq(EPI)) {
+            // acc_Q = sum_j ext_j ksk_j R^-1 (ext carries R), at the store
+            // position: acc_Q never makes an HBM round trip.  Each product is
+            // below 1.5q (2q generic), so one subtraction of 4q (WIDE) leaves
+            // the lazy sum below 4q; otherwise it is made canonical.
+            if (r + PD < R) {
+              const u32 kn = G0::k_reg(r + PD);
+#pragma unroll
+              for (int j = 0; j < KD; ++j) {
+                ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + j * ep.ext_j + kn, voff);
+                ek[(r + PD) % (PD + 1)][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
+              }
+            }
+            u64 e[KD], k[KD], pr[KD];
+#pragma unroll
+            for (int j = 0; j < KD; ++j) {
+              e[j] = ek[r % (PD + 1)][j];
+              k[j] = ek[r % (PD + 1)][KD + j];
+            }
+            if constexpr (SP) {
+              mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+            } else if constexpr (GEN_VEC) {
+              mont_mul_gen_vec<KD>(pr, e, k, mi);
+            } else {
+#pragma unroll
+              for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
+            }
+            acc = pr[0];
+            if constexpr (WIDE) {
+              // q < 2^60: the whole sum stays below 6q < 2^63
+#pragma unroll
+              for (int j = 1; j < KD; ++j) acc += pr[j];
+              if constexpr (KD > 2) acc = harvey_csub(acc, nq4);
+            } else {
+              // q < 2^61: keep the running sum below 2q, then canonical
+#pragma unroll
+              for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
+              acc = harvey_csub(acc, nq1);
+            }
+          } else {
+            acc = pa[r];
+          }
+          u64 ks = harvey_csub(mont_mul<SP>((acc + cb1) + ~v, ep.pinv, mi), nq1);
+          if (ep.add) ks = add_mod(ks, pb[r], q);
+          st_b(ep.out + kr, voff, ks);
+        } else {
+          st_b(data + kr, voff, v);
+        }
+      }
+    } else {
+      static_assert(!is_combine(EPI), "epilogues run in the re-laid-out row store");
+      // column pass (or single pass ending in group 0): element k of this
+      // thread sits at voff + k_reg(r) << LS -- a compile-time offset on the
+      // scalar base, so the address costs no VALU
+#pragma unroll
+      for (int r = 0; r < R; ++r) st_b(data + ((size_t)GP::k_reg(r) << PG::LS), voff, x[r]);
+    }
+  }
+}
+
+template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, bool WIDE, int EPI>
+__device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data, const u64 *tw, const ModInfo &mi,
+                                          u32 mod, u32 w, u32 ts, u32 hi, u32 gb, const EpiRow &ep) {
+  using PG = PassGeo<LOG_N, S, COLS, INV>;
+  constexpr int R = 1 << LOGR;
+  constexpr int NG = (S + LOGR - 1) / LOGR;
+  constexpr int G0 = INV ? NG - 1 : 0;
+  u64 tc[16];
+  Grp<S, LOGR, G0>::template load_tw<PG::S0>(tc, tw, hi, ts);
+  u64 x[R];
+  u32 voff;  // byte offset of this thread's element k_thr of the first (HBM) group layout
+  if constexpr (!COLS && G0 != 0) {
+    // row pass starting in a per-lane-contiguous group: coalesced load in the
+    // group-0 layout, then one LDS re-layout
+    using GZ = Grp<S, LOGR, 0>;
+    voff = (gb + GZ::k_thr(ts)) << 3;
+    if constexpr (EPI == PRO_TENSOR) {
+      // the CKKS tensor formulas, element-wise at the coalesced positions.
+      // Software-pipelined PD elements deep: the operand loads of element
+      // r + PD are issued before element r's stores (the outputs may alias the
+      // operands element-wise only, so the compiler would otherwise wait for
+      // each element's loads right after the previous element's stores)
+      constexpr int PD = SP ? 2 : 0;  // the generic products need the registers
+      u64 op[PD + 1][4];
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        const u32 kr = GZ::k_reg(r);
+        op[r][0] = ld_b(ep.a0 + kr, voff), op[r][1] = ld_b(ep.a1 + kr, voff);
+        op[r][2] = ld_b(ep.b0 + kr, voff), op[r][3] = ld_b(ep.b1 + kr, voff);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32 kr = GZ::k_reg(r);
+        if (r + PD < R) {
+          const u32 kn = GZ::k_reg(r + PD);
+          u64(&o)[4] = op[(r + PD) % (PD + 1)];
+          o[0] = ld_b(ep.a0 + kn, voff), o[1] = ld_b(ep.a1 + kn, voff);
+          o[2] = ld_b(ep.b0 + kn, voff), o[3] = ld_b(ep.b1 + kn, voff);
+        }
+        const u64 a0 = op[r % (PD + 1)][0], a1 = op[r % (PD + 1)][1];
+        const u64 b0 = op[r % (PD + 1)][2], b1 = op[r % (PD + 1)][3];
+        st_b(ep.o0 + kr, voff, mul_mod<SP>(a0, b0, mi));
+        U128 s = mul128(a0, b1);
+        mac128(s, a1, b0);
+        st_b(ep.o1 + kr, voff, reduce128<SP>(s, mi));
+        const u64 t = mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi);  // d2 in [0, 2q)
+        x[r] = csub(t, mi.q);
+        st_b(ep.ext + kr, voff, csub(mont_mul<SP>(t, mi.r2, mi), mi.q));  // d2 R
+      }
+    } else if constexpr (EPI == PRO_BFVT) {
+      // the BFV tensor formulas at the coalesced positions; e is per workgroup
+      if (ep.e == 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32 kr = GZ::k_reg(r);
+          U128 s = mul128(ld_b(ep.a0 + kr, voff), ld_b(ep.b1 + kr, voff));
+          mac128(s, ld_b(ep.a1 + kr, voff), ld_b(ep.b0 + kr, voff));
+          x[r] = reduce128<SP>(s, mi);
+        }
+      } else {
+        // e = 0: (a0, b0), e = 2: (a1, b1) -- the pair is resolved in ntt_pass
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32 kr = GZ::k_reg(r);
+          x[r] = mul_mod<SP>(ld_b(ep.a0 + kr, voff), ld_b(ep.b0 + kr, voff), mi);
+        }
+      }
+    } else if constexpr (EPI == PRO_AUTOMORPH) {
+      // NTT-domain automorphism (aut_src), software-pipelined like PRO_TENSOR:
+      // element r + PD's gathers are issued before element r's stores.  With
+      // o0 null, sigma(c0) is not stored (the combine reads it as sigma_g(c0))
+      constexpr int PD = AUT_PD;
+      const auto src_of = [&](int r) { return aut_src<LOG_N>((voff >> 3) + GZ::k_reg(r), ep.g); };
+      u64 y[PD + 1][2];
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        const u32 sr = src_of(r);
+        y[r][0] = ep.o0 ? ld_b(ep.a0, sr) : 0, y[r][1] = ld_b(ep.a1, sr);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32 kr = GZ::k_reg(r);
+        if (r + PD < R) {
+          const u32 sn = src_of(r + PD);
+          y[(r + PD) % (PD + 1)][0] = ep.o0 ? ld_b(ep.a0, sn) : 0, y[(r + PD) % (PD + 1)][1] = ld_b(ep.a1, sn);
+        }
+        const u64 y0 = y[r % (PD + 1)][0], y1 = y[r % (PD + 1)][1];
+        if (ep.o0) st_b(ep.o0 + kr, voff, y0);
+        x[r] = y1;
+        st_b(ep.ext + kr, voff, csub63(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
+      }
+    } else if constexpr (is_ksp(EPI)) {
+      // acc_P = sum_j ext_j ksk_j R^-1 (ks_inner_kernel; ext carries R) at the
+      // coalesced positions, canonical: the products are below 1.5q (2q
+      // generic), the running sum is kept below 2q.  Operands software-
+      // pipelined PD elements deep (as EPI_KSQ)
+      constexpr int KD = ksp_digits(EPI);
+      constexpr int PD = SP ? KSP_PD : 1;
+      u64 nq1 = 0 - mi.q, nq2 = 0 - 2 * mi.q;
+      asm("" : "+s"(nq1));
+      asm("" : "+s"(nq2));
+      u64 ek[PD + 1][2 * KD];
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        const u32 kr = GZ::k_reg(r);
+#pragma unroll
+        for (int j = 0; j < KD; ++j) {
+          ek[r][j] = ld_b(ep.kext + j * ep.ext_j + kr, voff);
+          ek[r][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r + PD < R) {
+          const u32 kn = GZ::k_reg(r + PD);
+#pragma unroll
+          for (int j = 0; j < KD; ++j) {
+            ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + j * ep.ext_j + kn, voff);
+            ek[(r + PD) % (PD + 1)][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
+          }
+        }
+        u64 e[KD], k[KD], pr[KD];
+#pragma unroll
+        for (int j = 0; j < KD; ++j) {
+          e[j] = ek[r % (PD + 1)][j];
+          k[j] = ek[r % (PD + 1)][KD + j];
+        }
+        if constexpr (SP) {
+          mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+        } else if constexpr (GEN_VEC) {
+          mont_mul_gen_vec<KD>(pr, e, k, mi);
+        } else {
+#pragma unroll
+          for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
+        }
+        u64 acc = pr[0];
+#pragma unroll
+        for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
+        x[r] = harvey_csub(acc, nq1);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[r] = ld_d(data + GZ::k_reg(r), voff);
+    }
+    const u32 lw = lds_idx<S>(w, GZ::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[lw + GZ::k_reg(r) + (GZ::k_reg(r) >> 4)] = x[r];
+    __syncthreads();
+    using GF = Grp<S, LOGR, G0>;
+    const u32 lr = lds_idx<S>(w, GF::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u32 kr = GF::k_reg(r);
+      x[r] = lds[lr + kr + (kr >> 4)];
+    }
+  } else {
+    using GF = Grp<S, LOGR, G0>;
+    voff = (gb + (GF::k_thr(ts) << PG::LS)) << 3;
+    if constexpr (is_conv(EPI)) {
+      // the base conversion (conv_apply, oracle) of this element from the NS
+      // source limbs at the same position, 4 elements at a time (NS is a
+      // template parameter: no per-term predication)
+      constexpr int NS = conv_ns(EPI);
+      constexpr size_t NW = (size_t)1 << LOG_N;
+      u32 hc0[NS], hc1[NS];  // the constants' 31-bit digits (uniform, SGPRs)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) split31(ep.h[i], hc0[i], hc1[i]);
+#pragma unroll
+      for (int c0 = 0; c0 < R; c0 += 4) {
+        u64 sv[4][NS];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < NS; ++i)
+            sv[j][i] = ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          x[c0 + j] = CONV_COLS && SP && WIDE && CONV_SP60 ? dot_cols_sp60<NS>(sv[j], hc0, hc1, mi.q_hi)  // < 2q
+                      : CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                                  // < 2q
+                                  : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);                   // < 4q
+      }
+    } else {
+      // the first forward pass may read out of place (NttArgs::src)
+      const u64 *din = data;
+      if constexpr (!INV && PG::S0 == 0)
+        if (a.src) din = a.src + (data - a.map.base);
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[r] = ld_d(din + ((size_t)GF::k_reg(r) << PG::LS), voff);
+    }
+  }
+  // the final store uses the group-0 layout for row passes and the last
+  // group's layout for column passes; recompute the offset for the latter
+  if constexpr (COLS) {
+    constexpr int GL = INV ? 0 : NG - 1;
+    voff = (gb + (Grp<S, LOGR, GL>::k_thr(ts) << PG::LS)) << 3;
+  } else {
+    voff = (gb + Grp<S, LOGR, 0>::k_thr(ts)) << 3;
+  }
+  group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, 0>(x, tc, lds, tw, data, voff, w, ts, hi, a, mi, mod, ep);
+}
+
+// PRO_CONV with CT target limbs per workgroup (round 4): the NS source words of
+// an element are loaded (and split into 31-bit digits) once and feed the CT
+// targets' dot products; target 0's transform runs while the other targets'
+// 16-word input tiles wait in VGPRs, then each following target's transform
+// starts from registers (no load phase).  One target per workgroup made every
+// target re-load all NS sources: NS L2 reads per element per target.
+template <int LOG_N, int S, int LOGR, int W, bool SP, bool WIDE, int EPI, int CT>
+__device__ __forceinline__ void conv_multi_body(const NttArgs &a, u64 *lds, u32 poly, u32 grp, u32 w, u32 ts,
+                                                u32 hi, u32 gb) {
+  using PG = PassGeo<LOG_N, S, true, false>;
+  constexpr int R = 1 << LOGR;
+  constexpr int NG = (S + LOGR - 1) / LOGR;
+  constexpr int NS = conv_ns(EPI);
+  constexpr size_t NW = (size_t)1 << LOG_N;
+  using GF = Grp<S, LOGR, 0>;
+  const u32 t0 = grp * CT;
+  const u32 nt = min((u32)CT, a.map.cnt - t0);  // uniform
+  u32 hc0[CT][NS], hc1[CT][NS];
+  u32 q_hi[CT];
+  ModInfo mt[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const u32 act = t0 + ((u32)t < nt ? t : 0);
+    mt[t] = a.mods[a.map.mod_offset + limbmap_limb(a.map, act)];
+    q_hi[t] = mt[t].q_hi;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) split31(a.c_h[(size_t)i * a.c_nd + act], hc0[t][i], hc1[t][i]);
+  }
+  const u64 *src = a.c_src + (((size_t)poly * a.c_src_stride + a.c_src_first) << LOG_N);
+  const u32 voff_in = (gb + (GF::k_thr(ts) << PG::LS)) << 3;
+  u64 x[CT][R];
+  // chunks of 4 elements (4 NS source words each), at most two chunks in
+  // flight: left alone the scheduler hoists all 16 NS loads (up to 226 VGPRs)
+  u64 sv[2][4][NS];
+  const auto load_chunk = [&](u64(&d)[4][NS], int c0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) d[j][i] = ld_b(src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff_in);
+  };
+  load_chunk(sv[0], 0);
+#pragma unroll
+  for (int k = 0; k < R / 4; ++k) {
+    if (k + 1 < R / 4) load_chunk(sv[(k + 1) & 1], 4 * (k + 1));
+#if CONV_PIPE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+        x[t][4 * k + j] = CONV_COLS && SP && WIDE && CONV_SP60
+                              ? dot_cols_sp60<NS>(sv[k & 1][j], hc0[t], hc1[t], q_hi[t])
+                              : dot_cols<NS, SP>(sv[k & 1][j], hc0[t], hc1[t], mt[t]);  // < 2q
+#if CONV_PIPE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
+  const u32 voff = (gb + (Grp<S, LOGR, NG - 1>::k_thr(ts) << PG::LS)) << 3;
+  const EpiRow ep{};
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    if ((u32)t >= nt) break;
+    if (t) __syncthreads();  // the previous target's last exchange has been read
+    const u32 limb = limbmap_limb(a.map, t0 + t);
+    const u32 mod = a.map.mod_offset + limb;
+    u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
+    const u64 *tw = a.tw + ((size_t)mod << LOG_N);
+    u64 tc[16];
+    Grp<S, LOGR, 0>::template load_tw<PG::S0>(tc, tw, hi, ts);
+    group_loop<LOG_N, S, LOGR, W, false, true, SP, WIDE, EPI_NONE, 0>(x[t], tc, lds, tw, data, voff, w, ts, hi, a,
+                                                                     mt[t], mod, ep);
+  }
+}
+
+
+#ifndef NTT_MINW
+#define NTT_MINW 1
+#endif
+#ifndef CONV_MINW
+#define CONV_MINW 4  // conv_multi_body: the LDS tile allows 4 waves per SIMD; without a bound the
+                     // compiler hoists every source load (130-226 VGPRs, 2-3 waves)
+#endif
+// WM (forward passes): the lazy schedule of the launch's moduli, chosen on the
+// host (wide_mode): 1 all WIDE (q < 2^60), 0 all narrow, 2 mixed (a per-
+// workgroup branch between both; the kernel then carries both code paths and
+// needs ~150 VGPRs instead of ~90, i.e. 3 waves per SIMD instead of the 4 the
+// LDS allows: a launch over one modulus class avoids it)
+template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int WM>
+__global__ void __launch_bounds__(W << (S - LOGR),
+                                  (W << (S - LOGR)) == 256 ? (is_conv(EPI) && CONV_T > 1 ? CONV_MINW : NTT_MINW) : 1)
+    ntt_pass(NttArgs a) {
+  static_assert(is_combine(EPI) || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
+                    EPI == PRO_BFVT || is_conv(EPI) || is_ksp(EPI),
+                "ntt_pass epilogues");
+  static_assert(!is_conv(EPI) || (!INV && COLS), "the conversion prologue feeds a forward column pass");
+  static_assert(!is_combine(EPI) || (!INV && !COLS), "epilogues follow a forward row pass");
+  static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT && !is_ksp(EPI)) || (INV && !COLS),
+                "prologues feed an inverse row pass");
+  using PG = PassGeo<LOG_N, S, COLS, INV>;
+  static_assert(!is_combine(EPI) || PG::LAST, "epilogues run in the last pass");
+  constexpr int T = 1 << (S - LOGR);
+  static_assert(LOGR == 4, "register tile is 16 words");
+  extern __shared__ u64 lds[];
+
+  // (poly, limb) come from gridDim.y / gridDim.z, so every per-workgroup
+  // quantity is scalar (SGPR) and element addresses are 32-bit offsets from a
+  // scalar base (global_load ... saddr): no 64-bit VALU address arithmetic
+  const u32 tid = threadIdx.x;
+  u32 bx = blockIdx.x, poly = blockIdx.y, act = blockIdx.z;
+  if constexpr (EPI == EPI_NONE) {
+    // every block of one job (poly, limb) on ONE XCD (ids are dealt
+    // round-robin over the 8 XCDs), jobs still in dispatch order: the blocks'
+    // row segments of one residue meet in one L2 (forward launch 2.07 ->
+    // 2.01 ms, profiles/r03/ab_xcd_job.txt)
+    const u32 nj = gridDim.y * gridDim.z;
+    if ((nj & 7) == 0) {
+      const u32 lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+      const u32 r = lin >> 3;
+      bx = r % gridDim.x;
+      const u32 j = (r / gridDim.x) * 8 + (lin & 7);
+      poly = j % gridDim.y;
+      act = j / gridDim.y;
+    }
+  }
+  if constexpr (is_ksq(EPI) || is_ksp(EPI)) {
+    // the 2 n polys (ct, b) of one (limb, row block) on consecutive workgroup
+    // ids of ONE XCD: the limb's key rows (2 dnum of them) stay in that XCD's
+    // L2 for the whole batch, and the b = 1 item re-reads the ext rows the
+    // b = 0 item just fetched
+    // GI groups are interleaved per XCD (their key rows all L2-resident)
+    constexpr u32 GIW = is_ksq(EPI) ? KSQ_GI : KSP_GI;
+    const u32 np = gridDim.y, lin = blockIdx.x + gridDim.x * (blockIdx.y + np * blockIdx.z);
+    const u32 r = lin >> 3, gpx = gridDim.x * gridDim.z / 8;  // groups per XCD
+    const u32 GI = gpx % GIW == 0 ? GIW : 1;
+    const u32 within = r % (GI * np);
+    const u32 g = ((r / (GI * np)) * GI + within % GI) * 8 + (lin & 7);  // g = (limb, row block)
+    poly = within / GI;
+    bx = g % gridDim.x;
+    act = g / gridDim.x;
+  }
+  if constexpr (is_conv(EPI)) {
+    // the T target limbs of one source block (poly, column block) run on
+    // consecutive workgroup ids of ONE XCD (ids are dealt round-robin over the
+    // 8 XCDs), so the ns source limbs come from that XCD's L2 after the first
+    // read instead of being re-fetched from HBM once per target
+    const u32 cbs = gridDim.x, T = gridDim.z, nsb = gridDim.x * gridDim.y;
+    const u32 lin = blockIdx.x + cbs * (blockIdx.y + gridDim.y * blockIdx.z);
+    u32 sb;
+    if ((nsb & 7) == 0) {
+      const u32 rest = lin >> 3;
+      act = rest % T;
+      sb = (rest / T) * 8 + (lin & 7);
+    } else {
+      act = lin % T;
+      sb = lin / T;
+    }
+    bx = sb % cbs;
+    poly = sb / cbs;
+    if constexpr (CONV_T > 1) {
+      // act = target group (CONV_T target limbs)
+      u32 w = tid % W, ts = tid / W;
+      constexpr u32 stride = 1u << PG::LS;
+      const u32 u = bx * W + w;
+      const u32 hi = u >> PG::LS;
+      const u32 gb = (hi << (S + PG::LS)) + (u & (stride - 1));
+      // mixed moduli classes (WM 2) take the narrow schedule, valid for every target
+      constexpr bool WIDE_C = !INV && WM == 1;
+      conv_multi_body<LOG_N, S, LOGR, W, SP, WIDE_C, EPI, CONV_T>(a, lds, poly, act, w, ts, hi, gb);
+      return;
+    }
+  }
+  const u32 limb = limbmap_limb(a.map, act);
+  const u32 mod = a.map.mod_offset + limb;
+  u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
+  const ModInfo mi = a.mods[mod];
+  const u64 *tw = a.tw + ((size_t)mod << LOG_N);
+  constexpr u32 stride = 1u << PG::LS;
+
+  // column passes put the W sub-transforms (adjacent columns) on adjacent
+  // lanes: every wave access is four 128 B row segments
+  u32 w, ts;
+  if (COLS) { w = tid % W; ts = tid / W; } else { ts = tid % T; w = tid / T; }
+  const u32 u = bx * W + w;
+  const u32 hi = u >> PG::LS;
+  const u32 gb = (hi << (S + PG::LS)) + (u & (stride - 1));
+
+  EpiRow ep{};
+  if constexpr (is_ksp(EPI)) {
+    const size_t N = (size_t)1 << LOG_N;
+    ep.ext_j = (size_t)a.e_QP * N;
+    ep.ksk_j = 2 * ep.ext_j;
+    ep.kext = a.e_ext + ((size_t)(poly >> 1) * a.e_ndig * a.e_QP + limb) * N;
+    ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_QP + limb) * N;
+  }
+  if constexpr (is_combine(EPI)) {
+    if constexpr (is_ksq(EPI)) {
+      const size_t N = (size_t)1 << LOG_N;
+      ep.ext_j = (size_t)a.e_QP * N;
+      ep.ksk_j = 2 * ep.ext_j;
+      ep.kext = a.e_ext + ((size_t)(poly >> 1) * a.e_ndig * a.e_QP + limb) * N;
+      ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_QP + limb) * N;
+    }
+    ep.acc = a.e_acc + (((size_t)poly * a.e_acc_stride + limb) << LOG_N);
+    ep.base = a.e_base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
+    ep.out = a.e_out + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
+    ep.pinv = a.e_pinv[limb];
+    ep.add = (a.e_add_mask >> (poly & 1)) & 1;
+    ep.g = a.e_g;
+  }
+  if constexpr (EPI == PRO_TENSOR) {
+    const size_t LN = (size_t)a.t_L << LOG_N;
+    const size_t o = ((size_t)poly * 2 * a.t_L + limb) << LOG_N;
+    ep.a0 = a.t_a + o;
+    ep.a1 = ep.a0 + LN;
+    ep.b0 = a.t_b + o;
+    ep.b1 = ep.b0 + LN;
+    ep.o0 = a.t_out + o;
+    ep.o1 = ep.o0 + LN;
+    ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
+  }
+  if constexpr (EPI == PRO_BFVT) {
+    // poly = 3 ct + e; the inputs are t_a, t_b [ct][2][nl][N] = (a0, a1), (b0, b1)
+    const size_t LN = (size_t)a.t_L << LOG_N;
+    const size_t o = ((size_t)(poly / 3) * 2 * a.t_L + limb) << LOG_N;
+    const u64 *xa = a.t_a + o, *xb = a.t_b + o;
+    ep.e = poly % 3;
+    ep.a0 = ep.e == 2 ? xa + LN : xa;
+    ep.a1 = xa + LN;
+    ep.b0 = ep.e == 2 ? xb + LN : xb;
+    ep.b1 = xb + LN;
+  }
+  if constexpr (EPI == PRO_AUTOMORPH) {
+    const size_t LN = (size_t)a.t_L << LOG_N;
+    const size_t o = ((size_t)poly * 2 * a.t_L + limb) << LOG_N;
+    ep.a0 = a.t_a + o;
+    ep.a1 = ep.a0 + LN;
+    ep.o0 = a.t_out ? a.t_out + o : nullptr;
+    ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
+    ep.g = a.t_g;
+  }
+  if constexpr (is_conv(EPI)) {
+    ep.src = a.c_src + (((size_t)poly * a.c_src_stride + a.c_src_first) << LOG_N);
+#pragma unroll
+    for (int i = 0; i < conv_ns(EPI); ++i) ep.h[i] = a.c_h[(size_t)i * a.c_nd + act];
+  }
+  if constexpr (!INV && WM == 2) {
+    // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)
+    if (mi.q < (1ull << 60)) {
+      pass_body<LOG_N, S, LOGR, W, INV, COLS, SP, true, EPI>(a, lds, data, tw, mi, mod, w, ts, hi, gb, ep);
+      return;
+    }
+  }
+  pass_body<LOG_N, S, LOGR, W, INV, COLS, SP, !INV && WM == 1, EPI>(a, lds, data, tw, mi, mod, w, ts, hi, gb, ep);
+}
+
+// lazy-schedule class of the moduli a launch over map m touches (ntt_pass WM)
+[[maybe_unused]] int wide_mode(const fhe_ctx *c, const LimbMap &m) {
+  bool wide = false, narrow = false;
+  for (u32 act = 0; act < m.cnt; ++act) {
+    const u64 q = c->moduli[m.mod_offset + limbmap_limb(m, act)];
+    (q < (1ull << 60) ? wide : narrow) = true;
+  }
+  return wide && narrow ? 2 : wide ? 1 : 0;
+}
+
+template <int LOG_N, int S, int W, bool COLS, bool INV, bool SP, int EPI, int WM = 0>
+int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
+  constexpr int LOGR = 4;
+  constexpr int NT = W << (S - LOGR);
+  constexpr size_t lds = lds_bytes<S, W>();
+  constexpr u32 subs = 1u << (LOG_N - S);
+  // dispatch order: row blocks, then polys, then limbs -- the resident
+  // workgroups share one modulus, so its twiddle table stays in L2
+  // (conversion prologue: gridDim.z counts groups of CONV_T target limbs)
+  dim3 grid(subs / W, n_jobs / a.map.cnt, is_conv(EPI) ? (a.map.cnt + CONV_T - 1) / CONV_T : a.map.cnt);
+  auto k = ntt_pass<LOG_N, S, LOGR, W, INV, COLS, SP, EPI, WM>;
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);
+  return fhe_check(c, hipGetLastError(), "ntt_pass launch");
+}
+
+// a forward pass, with the lazy schedule class of its moduli
+template <int LOG_N, int S, int W, bool COLS, int EPI, bool SP>
+int launch_fwd(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
+  switch (wide_mode(c, a.map)) {
+    case 1: return launch_one<LOG_N, S, W, COLS, false, SP, EPI, 1>(c, a, n_jobs);
+    case 0: return launch_one<LOG_N, S, W, COLS, false, SP, EPI, 0>(c, a, n_jobs);
+  }
+  return launch_one<LOG_N, S, W, COLS, false, SP, EPI, 2>(c, a, n_jobs);
+}
+
+template <int LOG_N, int S, int W, bool COLS, int EPI = EPI_NONE>
+int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  if constexpr (is_combine(EPI) || is_conv(EPI)) {
+    if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
+    return c->special ? launch_fwd<LOG_N, S, W, COLS, EPI, true>(c, a, n_jobs)
+                      : launch_fwd<LOG_N, S, W, COLS, EPI, false>(c, a, n_jobs);
+  } else if constexpr (EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH || EPI == PRO_BFVT || is_ksp(EPI)) {
+    if (!inv) return fhe_fail(c, FHE_ERR_INVALID, "prologue on a forward pass");
+    return c->special ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
+                      : launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs);
+  } else {
+    if (c->special)
+      return inv ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
+                 : launch_fwd<LOG_N, S, W, COLS, EPI, true>(c, a, n_jobs);
+    return inv ? launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs)
+               : launch_fwd<LOG_N, S, W, COLS, EPI, false>(c, a, n_jobs);
+  }
+}
+
+// one pass over a whole residue (N <= 2^14)
+template <int EPI = EPI_NONE>
+int single_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  switch (a.log_n) {
+    case 10: return launch_pass<10, 10, 1, false, EPI>(c, a, inv, n_jobs);
+    case 11: return launch_pass<11, 11, 1, false, EPI>(c, a, inv, n_jobs);
+    case 12: return launch_pass<12, 12, 1, false, EPI>(c, a, inv, n_jobs);
+    case 13: return launch_pass<13, 13, 1, false, EPI>(c, a, inv, n_jobs);
+    case 14: return launch_pass<14, 14, 1, false, EPI>(c, a, inv, n_jobs);
+  }
+  return fhe_fail(c, FHE_ERR_UNSUPPORTED, "single_pass: log_n");
+}
+
+// column pass: stages [0, S1), stride N >> S1
+template <int EPI = EPI_NONE>
+int col_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  if constexpr (EPI == EPI_NONE)
+    if (a.log_n == 14) return launch_pass<14, 7, 32, true, EPI>(c, a, inv, n_jobs);
+  switch (a.log_n) {
+    case 15: return launch_pass<15, 7, 32, true, EPI>(c, a, inv, n_jobs);
+    case 16: return launch_pass<16, 8, 16, true, EPI>(c, a, inv, n_jobs);
+    case 17: return launch_pass<17, 8, 16, true, EPI>(c, a, inv, n_jobs);
+  }
+  return fhe_fail(c, FHE_ERR_UNSUPPORTED, "col_pass: log_n");
+}
+
+// row pass: stages [S1, logN), contiguous blocks
+template <int EPI = EPI_NONE>
+int row_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  if constexpr (EPI == EPI_NONE)
+    if (a.log_n == 14) return launch_pass<14, 7, 32, false, EPI>(c, a, inv, n_jobs);
+  switch (a.log_n) {
+    case 15: return launch_pass<15, 8, 16, false, EPI>(c, a, inv, n_jobs);
+    case 16: return launch_pass<16, 8, 16, false, EPI>(c, a, inv, n_jobs);
+    case 17: return launch_pass<17, 9, 8, false, EPI>(c, a, inv, n_jobs);
+  }
+  return fhe_fail(c, FHE_ERR_UNSUPPORTED, "row_pass: log_n");
+}
+
+}  // namespace

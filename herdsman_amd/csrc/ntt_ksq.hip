@@ -1,0 +1,73 @@
+// ntt_ksq.hip -- NTT(conv) with the ModDown finish (EPI_COMBINE) and the Q-limb inner product (EPI_KSQ)
+// (kernel templates: ntt_core.hpp; one translation unit per entry-point family so
+// the ~360 pass kernels compile in parallel)
+#include "ntt_core.hpp"
+
+// Forward NTT of the ModDown conversion conv (all L limbs of 2n polys) with
+// the ModDown finish fused into its last pass (EPI_COMBINE):
+//   out[p][i] = (add_mask bit (p & 1) ? base[p][i] : 0) + (acc[p][i] - NTT(conv)[p][i]) P^-1  mod q_i
+// conv is transformed in place by the first pass only; acc rows have stride acc_stride limbs.
+// With ext (EPI_KSQ, two-pass sizes) acc's Q limbs are not read: the last pass
+// forms acc[2 ct + b][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1 itself.
+int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
+                           u64 *out, u32 add_mask, const ConvTab *pro, const u64 *ext, const u64 *ksk, u32 ndig,
+                           u32 base_g) {
+  const u32 L = c->L, QP = c->L + c->K;
+  const size_t N = c->n;
+  if (ext && (c->log_n <= 14 || ndig > 4 || (n_polys & 1)))
+    return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch inner product: log_n / digits");
+  if (base_g && c->log_n <= 14) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated combine base: log_n");
+  const u32 per = COMBINE_CHUNK;  // polys per pass pair: gridDim.y, even (the polys of a ciphertext stay together)
+  for (u32 p0 = 0; p0 < n_polys; p0 += per) {
+    const u32 np = std::min(per, n_polys - p0);
+    NttArgs a{};
+    a.map = LimbMap{conv + (size_t)p0 * L * N, L, L, 0, L, 0, 0, np};
+    a.tw = c->d_tw_fwd;
+    a.mods = c->d_mods;
+    a.ninv = c->d_ninv;
+    a.log_n = c->log_n;
+    a.e_acc = acc + (size_t)p0 * acc_stride * N;
+    a.e_base = base + (size_t)p0 * L * N;
+    a.e_out = out + (size_t)p0 * L * N;
+    a.e_pinv = c->d_pinv;
+    a.e_acc_stride = acc_stride;
+    a.e_add_mask = add_mask;
+    a.e_g = base_g & ((2u << c->log_n) - 1);
+    if (ext) {
+      a.e_ext = ext + (size_t)(p0 / 2) * ndig * QP * N;
+      a.e_ksk = ksk;
+      a.e_ndig = ndig;
+      a.e_QP = QP;
+    }
+    const u32 n_jobs = np * L;
+    int rc;
+    if (c->log_n <= 14) {
+      rc = single_pass<EPI_COMBINE>(c, a, false, n_jobs);
+    } else {
+      if (pro) {
+        // the ModDown conversion P -> Q as the column pass's prologue: the
+        // sources are acc's P limbs, already scaled by the INTT (d_iscale)
+        a.c_src = acc + (size_t)p0 * acc_stride * N;
+        a.c_src_stride = acc_stride;
+        a.c_src_first = L;
+        a.c_ns = pro->ns;
+        a.c_nd = pro->nd;
+        a.c_h = pro->h;
+        rc = ntt_conv_col(c, a, n_jobs);
+      } else {
+        rc = ntt_col_plain(c, a, false, n_jobs);
+      }
+      if (rc) return rc;
+      switch (ext ? ndig : 0) {
+        case 1: rc = row_pass<EPI_KSQ>(c, a, false, n_jobs); break;
+        case 2: rc = row_pass<EPI_KSQ + 1>(c, a, false, n_jobs); break;
+        case 3: rc = row_pass<EPI_KSQ + 2>(c, a, false, n_jobs); break;
+        case 4: rc = row_pass<EPI_KSQ + 3>(c, a, false, n_jobs); break;
+        default: rc = row_pass<EPI_COMBINE>(c, a, false, n_jobs);
+      }
+    }
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+

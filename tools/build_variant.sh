@@ -16,9 +16,9 @@ fi
 sed -i "s@\"../../include/plugins/fhe_backend.h\"@\"plugins/fhe_backend.h\"@" "$D"/csrc/*.hpp "$D"/csrc/*.cpp "$D"/csrc/*.hip
 while [ $# -ge 2 ]; do sed -i "$1" "$D/csrc/$2"; shift 2; done
 cd "$D"
-for f in ntt rns; do /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" $EXTRA -c -o $f.o csrc/$f.hip & done
+for f in csrc/*.hip; do b=$(basename "$f" .hip); /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" $EXTRA -c -o $b.o "$f" & done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" -x hip -c -o be.o csrc/fhe_backend.cpp &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o libherdsman_fhe.so ntt.o rns.o be.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o libherdsman_fhe.so *.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f *.o
 echo "built $D/libherdsman_fhe.so"

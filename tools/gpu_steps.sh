@@ -1,0 +1,31 @@
+#!/bin/bash
+# One parameterised GPU-box driver (replaces the round-3 one-off gpu_cmd_*.sh scripts).
+#   gpurun -- 'bash tools/gpu_steps.sh OUT step [step ...]'
+# Steps (each under its own time limit; the first failure ends the run):
+#   suite          pytest -m gpu (the whole GPU suite)
+#   test=EXPR      pytest -m gpu -k EXPR
+#   smoke          __graft_entry__.smoke()
+#   bench          the default bench.py line (CPU baseline and secondaries included)
+#   quick          bench.py --no-cpu --no-secondary --steps 3 --warmup 1
+#   ab=V1,V2,...   tools/ab_quick.sh over library variants ("main" = herdsman_amd/lib)
+#   stats          rocprofv3 --kernel-trace --stats of a short bench.py (roofline summary)
+#   steptable      rocprofv3 kernel trace of one C5 wave loop -> tools/step_table.py
+set -e
+export TMPDIR=/tmp
+O=$1; shift
+mkdir -p "$O"
+for s in "$@"; do
+  echo "== $s $(date +%T)"
+  case $s in
+    suite) timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/gputests.log" 2>&1 ;;
+    test=*) timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${s#test=}" > "$O/gputest_${s#test=}.log" 2>&1 ;;
+    smoke) timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 600 python3 bench.py > "$O/bench.log" 2>&1 ;;
+    quick) timeout -k 10 300 python3 bench.py --no-cpu --no-secondary --steps 3 --warmup 1 > "$O/quick.log" 2>&1 ;;
+    ab=*) IFS=, read -r -a vs <<< "${s#ab=}"; bash tools/ab_quick.sh "$O/q" "${vs[@]}" > "$O/ab.txt" 2>&1 ;;
+    stats) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/stats" -o run -- python3 bench.py --no-cpu --no-secondary --steps 3 --warmup 1 > "$O/stats.log" 2>&1 ;;
+    steptable) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/step" -o run -- python3 tools/op_bench.py ckks_mul --batch 128 --reps 8 > "$O/step.log" 2>&1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
