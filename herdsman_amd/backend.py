@@ -77,6 +77,12 @@ SIGNATURES = {
     "fhe_keyswitch": (C.c_int, [_vp, _vp, _vp, _vp, _u32]),
     "fhe_rotate": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _u32]),
     "fhe_galois_elt": (C.c_int, [_vp, _i32, C.POINTER(_u32)]),
+    "fhe_add_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
+    "fhe_sub_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
+    "fhe_mul_relin_at": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _u32, _u32]),
+    "fhe_rotate_at": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _u32, _u32]),
+    "fhe_keyswitch_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
+    "fhe_rescale": (C.c_int, [_vp, _vp, _vp, _u32, _u32]),
     "fhe_reduce": (C.c_int, [_vp, _vp, _u32, C.c_int, _vp, _vp]),
     "fhe_bcast_key": (C.c_int, [_vp, _vp, _sz, _vp, C.c_int]),
     "fhe_reduce_ranks": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, C.c_int, _vp]),
@@ -284,6 +290,61 @@ class Context:
         n = self._ct_batch(ct, out)
         self._key(gk)
         self._ck(self.lib.fhe_rotate(self.h, _ptr(ct), galois, _ptr(gk), _ptr(out), n), "fhe_rotate")
+        return out
+
+    # ---- CKKS levels: ciphertexts [n][2][level][N] over the first `level` Q primes
+    def _ct_level(self, level: int, *cts):
+        if not 1 <= level <= self.L:
+            raise FheBackendError(f"level {level} outside [1, {self.L}]")
+        n = cts[0].shape[0] if cts[0].dim() == 4 else -1
+        want = (n, 2, level, self.n)
+        for t in cts:
+            if tuple(t.shape) != want:
+                raise FheBackendError(f"level-{level} ciphertext batch shape {tuple(t.shape)}, expected {want}")
+        self._on_device(*cts)
+        return n
+
+    def add_at(self, a, b, out, level: int):
+        n = self._ct_level(level, a, b, out)
+        self._ck(self.lib.fhe_add_at(self.h, _ptr(a), _ptr(b), _ptr(out), n, level), "fhe_add_at")
+        return out
+
+    def sub_at(self, a, b, out, level: int):
+        n = self._ct_level(level, a, b, out)
+        self._ck(self.lib.fhe_sub_at(self.h, _ptr(a), _ptr(b), _ptr(out), n, level), "fhe_sub_at")
+        return out
+
+    def mul_relin_at(self, a, b, rlk, out, level: int):
+        n = self._ct_level(level, a, b, out)
+        self._key(rlk)
+        self._ck(self.lib.fhe_mul_relin_at(self.h, _ptr(a), _ptr(b), _ptr(rlk), _ptr(out), n, level),
+                 "fhe_mul_relin_at")
+        return out
+
+    def rotate_at(self, ct, galois: int, gk, out, level: int):
+        n = self._ct_level(level, ct, out)
+        self._key(gk)
+        self._ck(self.lib.fhe_rotate_at(self.h, _ptr(ct), galois, _ptr(gk), _ptr(out), n, level), "fhe_rotate_at")
+        return out
+
+    def keyswitch_at(self, d, ksk, out, level: int):
+        n = self._ct_level(level, out)
+        if tuple(d.shape) != (n, level, self.n):
+            raise FheBackendError(f"keyswitch input shape {tuple(d.shape)}, expected {(n, level, self.n)}")
+        self._on_device(d)
+        self._key(ksk)
+        self._ck(self.lib.fhe_keyswitch_at(self.h, _ptr(d), _ptr(ksk), _ptr(out), n, level), "fhe_keyswitch_at")
+        return out
+
+    def rescale(self, ct, out, level: int):
+        """level -> level - 1: out [n][2][level-1][N] = round(ct / q_{level-1})."""
+        n = self._ct_level(level, ct)
+        if level < 2:
+            raise FheBackendError("rescale needs level >= 2")
+        self._ct_level(level - 1, out)
+        if out.shape[0] != ct.shape[0]:
+            raise FheBackendError("rescale: input and output batch sizes differ")
+        self._ck(self.lib.fhe_rescale(self.h, _ptr(ct), _ptr(out), n, level), "fhe_rescale")
         return out
 
     def reduce(self, cts, op: int, rlk=None, out=None):

@@ -92,7 +92,25 @@ struct fhe_ctx {
   size_t ws_bytes = 0;
   // fhe_mark / fhe_wait_mark events, created on first use
   hipEvent_t marks[FHE_MAX_MARKS] = {};
+  // ---- CKKS levels (fhe_*_at, fhe_rescale).  A ciphertext at level m < L has
+  // the first m Q limbs; its ops run on a LEVEL VIEW: a context over the moduli
+  // Q_m u P (index space [0,m) = Q_m, [m,m+K) = P) with the parent's alpha, so
+  // the digits partition the m active limbs (the last one possibly partial).
+  // Views are built on first use, share the parent's stream and workspace and
+  // are destroyed with it.  Switching keys stay in the full-level layout
+  // [dnum][2][L+K][N]: view limb i reads key row i (Q) or i + key_pshift (P).
+  fhe_ctx *parent = nullptr;
+  std::vector<fhe_ctx *> views;  // [m] = view at level m (1 <= m < L), null until used
+  u32 key_qp = 0;                // key rows per digit half (0: L + K)
+  u32 key_pshift = 0;            // L_parent - m for a view
+  u64 *d_qdrop = nullptr;        // view at level m: [2m] = q_m^-1 R mod q_i, then q_m mod q_i (rescale m+1 -> m)
 };
+
+// key layout of a context (level views read the parent's full-level keys)
+inline u32 ctx_key_qp(const fhe_ctx *c) { return c->key_qp ? c->key_qp : c->L + c->K; }
+// *out = the context of level m (1 <= m <= L): c's root itself for m = L, else
+// its view (built on first use); an FHE_ERR_* code with c->err set on failure
+int ctx_level(fhe_ctx *c, u32 m, fhe_ctx **out);
 
 // Binds the context's device for the duration of an ABI call and restores the
 // caller's current device: a host thread may drive contexts on several GPUs,
@@ -113,9 +131,16 @@ struct DeviceBind {
 // The same for a bare device id (context creation and destruction).
 struct DeviceIdBind {
   int prev = -1;
+  bool ok = true;  // dev is the current device (fhe_ctx_create fails with FHE_ERR_DEVICE otherwise)
   explicit DeviceIdBind(int dev) {
-    if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
-    else prev = -1;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) {
+      ok = hipSetDevice(dev) == hipSuccess;  // nothing to restore
+      return;
+    }
+    if (cur == dev) return;
+    ok = hipSetDevice(dev) == hipSuccess;
+    if (ok) prev = cur;
   }
   ~DeviceIdBind() {
     if (prev >= 0) (void)hipSetDevice(prev);
@@ -146,9 +171,10 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false,
 // the column pass (PRO_CONV); null = conv already holds the converted limbs
 // ext / ksk: acc's Q limbs are the key-switching inner product of ext [n][ndig][QP][N]
 // with ksk [ndig][2][QP][N], formed in the last pass instead of read (EPI_KSQ)
+// pinv: the epilogue's per-limb constant (null: P^-1, d_pinv; rescale: q_last^-1, d_qdrop)
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro = nullptr, const u64 *ext = nullptr,
-                           const u64 *ksk = nullptr, u32 ndig = 0, u32 base_g = 0);
+                           const u64 *ksk = nullptr, u32 ndig = 0, u32 base_g = 0, const u64 *pinv = nullptr);
 // ModUp of digit j fused into the column pass of the forward NTT of its
 // converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
@@ -170,6 +196,10 @@ int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u
                  u32 add_mask, bool ntt_form, u64 *ws);
 int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n);
 int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n, bool ntt_form);
+// CKKS rescale of n ciphertexts of level m + 1 (on `up`, the context of level
+// m + 1) to level m (on `lo`, the context of level m); ct must not overlap out
+int rescale_impl(fhe_ctx *up, fhe_ctx *lo, const u64 *ct, u64 *out, u32 n);
+size_t rescale_ws_bytes(const fhe_ctx *lo, u32 n);
 int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n_ct);
 int behz_setup(fhe_ctx *c);
 size_t keyswitch_ws_bytes(const fhe_ctx *c, u32 n);

@@ -3,6 +3,7 @@
 // live in ntt.hip / rns.hip.  Nothing here computes on the CPU what the ABI
 // promises to compute on the GPU: host work is limited to one-off table
 // generation at context creation (primes, roots, CRT constants).
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -112,20 +113,22 @@ void *ctx_upload(fhe_ctx *c, const void *host, size_t bytes) {
   c->blobs.push_back(p);
   return p;
 }
+// level views use their parent's workspace (they run on its stream)
 int ctx_workspace(fhe_ctx *c, size_t bytes, void **out) {
-  if (bytes > c->ws_bytes) {
-    if (c->ws) {
+  fhe_ctx *o = c->parent ? c->parent : c;
+  if (bytes > o->ws_bytes) {
+    if (o->ws) {
       int rc = fhe_check(c, hipStreamSynchronize(c->stream), "workspace sync");
       if (rc) return rc;
-      (void)hipFree(c->ws);
-      c->ws = nullptr;
-      c->ws_bytes = 0;
+      (void)hipFree(o->ws);
+      o->ws = nullptr;
+      o->ws_bytes = 0;
     }
-    int rc = fhe_check(c, hipMalloc(&c->ws, bytes), "workspace alloc");
+    int rc = fhe_check(c, hipMalloc(&o->ws, bytes), "workspace alloc");
     if (rc) return rc;
-    c->ws_bytes = bytes;
+    o->ws_bytes = bytes;
   }
-  *out = c->ws;
+  *out = o->ws;
   return FHE_OK;
 }
 
@@ -162,6 +165,12 @@ ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector
 
 static void ctx_release(fhe_ctx *c) {
   if (!c) return;
+  for (fhe_ctx *v : c->views)
+    if (v) {
+      ctx_release(v);
+      delete v;
+    }
+  c->views.clear();
   for (void *p : c->blobs) (void)hipFree(p);
   c->blobs.clear();
   c->conv_cache.clear();
@@ -176,7 +185,9 @@ static void ctx_release(fhe_ctx *c) {
 }
 
 // ------------------------------------------------------------ context
-static int ctx_build(fhe_ctx *c, const fhe_params *p) {
+// alpha: digit size override (level views keep their parent's alpha, which
+// ceil(m / dnum_m) need not reproduce)
+static int ctx_build(fhe_ctx *c, const fhe_params *p, u32 alpha = 0) {
   c->params = *p;
   c->params.moduli = nullptr;
   c->log_n = p->log_n;
@@ -184,7 +195,7 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
   c->L = p->num_q;
   c->K = p->num_p;
   c->dnum = p->dnum;
-  c->alpha = (c->L + c->dnum - 1) / c->dnum;
+  c->alpha = alpha ? alpha : (c->L + c->dnum - 1) / c->dnum;
   c->t = p->plain_modulus;
   c->nB = p->scheme == FHE_SCHEME_BFV ? c->L + 1 : 0;
   c->nmod = c->L + c->K + c->nB;
@@ -307,6 +318,59 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p) {
   return FHE_OK;
 }
 
+// ------------------------------------------------------------ level views
+int ctx_level(fhe_ctx *c, u32 m, fhe_ctx **out) {
+  fhe_ctx *r = c->parent ? c->parent : c;
+  *out = nullptr;
+  if (m == r->L) {
+    *out = r;
+    return FHE_OK;
+  }
+  if (r->params.scheme != FHE_SCHEME_CKKS) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "reduced levels are CKKS only");
+  if (m < 1 || m > r->L) return fhe_fail(c, FHE_ERR_INVALID, "level must be in [1, L]");
+  if (r->views.size() < r->L) r->views.resize(r->L, nullptr);
+  fhe_ctx *v = r->views[m];
+  if (!v) {
+    v = new (std::nothrow) fhe_ctx();
+    if (!v) return fhe_fail(c, FHE_ERR_OOM, "level view");
+    v->parent = r;
+    v->device = r->device;
+    v->stream = r->stream;
+    fhe_params p = r->params;
+    std::vector<u64> mods(r->moduli.begin(), r->moduli.begin() + m);
+    mods.insert(mods.end(), r->moduli.begin() + r->L, r->moduli.begin() + r->L + r->K);
+    p.num_q = m;
+    p.dnum = (m + r->alpha - 1) / r->alpha;
+    p.moduli = mods.data();
+    int rc = ctx_build(v, &p, r->alpha);
+    if (!rc) {
+      v->key_qp = r->L + r->K;
+      v->key_pshift = r->L - m;
+      // rescale m+1 -> m: q_m^-1 R mod q_i, then q_m mod q_i (i < m)
+      const u64 qm = r->moduli[m];
+      std::vector<u64> qd(2 * (size_t)m);
+      for (u32 i = 0; i < m; ++i) {
+        const u64 qi = r->moduli[i];
+        qd[i] = tomont(hinv(qm % qi, qi), qi);
+        qd[m + i] = qm % qi;
+      }
+      v->d_qdrop = (u64 *)ctx_upload(v, qd.data(), sizeof(u64) * qd.size());
+      if (!v->d_qdrop) rc = fhe_fail(v, FHE_ERR_OOM, "level view tables");
+    }
+    if (rc) {
+      fhe_fail(c, rc, "level view: " + v->err);
+      ctx_release(v);
+      delete v;
+      return rc;
+    }
+    r->views[m] = v;
+  }
+  v->stream = r->stream;
+  v->err.clear();
+  *out = v;
+  return FHE_OK;
+}
+
 static thread_local std::string g_create_error;
 
 extern "C" {
@@ -321,6 +385,10 @@ int fhe_ctx_create(const fhe_params *params, int device, fhe_ctx **out) {
   }
   if (device < 0 || device >= ndev) return FHE_ERR_INVALID;
   DeviceIdBind bind(device);  // the caller's current device is restored on return
+  if (!bind.ok) {
+    g_create_error = "hipSetDevice failed";
+    return FHE_ERR_DEVICE;
+  }
   fhe_ctx *c = new (std::nothrow) fhe_ctx();
   if (!c) return FHE_ERR_OOM;
   c->device = device;
@@ -369,7 +437,14 @@ int fhe_mark(fhe_ctx *c, uint32_t slot) {
   if (slot >= FHE_MAX_MARKS) return fhe_fail(c, FHE_ERR_INVALID, "mark slot out of range");
   DeviceBind bind(c);
   if (!c->marks[slot]) {
-    int rc = fhe_check(c, hipEventCreateWithFlags(&c->marks[slot], hipEventDisableTiming), "mark create");
+    // blocking sync: a lane thread waiting on a batch sleeps instead of spinning
+    // against the lanes' IO threads (HERD_FHE_SPIN_WAIT=1 keeps the spin wait)
+    static const bool spin = [] {
+      const char *e = getenv("HERD_FHE_SPIN_WAIT");
+      return e && e[0] == '1';
+    }();
+    const unsigned flags = hipEventDisableTiming | (spin ? 0u : hipEventBlockingSync);
+    int rc = fhe_check(c, hipEventCreateWithFlags(&c->marks[slot], flags), "mark create");
     if (rc) return rc;
   }
   return fhe_check(c, hipEventRecord(c->marks[slot], c->stream), "mark record");
@@ -583,6 +658,69 @@ int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, u
   for (uint32_t c0 = 0; c0 < n_ct; c0 += kCtChunk) {
     const uint32_t m = std::min(kCtChunk, n_ct - c0);
     if ((rc = rotate_impl(c, ct + c0 * cw, g, gk, out + c0 * cw, m, c->params.scheme == FHE_SCHEME_CKKS))) return rc;
+  }
+  return FHE_OK;
+}
+
+// ---- CKKS levels: the op of the level-m view, its error reported on c
+static int at_level(fhe_ctx *c, uint32_t level, fhe_ctx **v) {
+  if (!c) return FHE_ERR_INVALID;
+  return ctx_level(c, level, v);
+}
+static int from_view(fhe_ctx *c, fhe_ctx *v, int rc) {
+  if (rc && v != c) c->err = v->err;
+  return rc;
+}
+
+int fhe_add_at(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct, uint32_t level) {
+  if (!c) return FHE_ERR_INVALID;
+  if (level == 0 || level > c->L) return fhe_fail(c, FHE_ERR_INVALID, "level must be in [1, L]");
+  return ew(c, EwOp::Add, a, b, out, 2 * n_ct, 0, level);
+}
+int fhe_sub_at(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct, uint32_t level) {
+  if (!c) return FHE_ERR_INVALID;
+  if (level == 0 || level > c->L) return fhe_fail(c, FHE_ERR_INVALID, "level must be in [1, L]");
+  return ew(c, EwOp::Sub, a, b, out, 2 * n_ct, 0, level);
+}
+int fhe_mul_relin_at(fhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk, uint64_t *out,
+                     uint32_t n_ct, uint32_t level) {
+  fhe_ctx *v;
+  DeviceBind bind(c);
+  int rc = at_level(c, level, &v);
+  return rc ? rc : from_view(c, v, fhe_mul_relin(v, a, b, rlk, out, n_ct));
+}
+int fhe_rotate_at(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out, uint32_t n_ct,
+                  uint32_t level) {
+  fhe_ctx *v;
+  DeviceBind bind(c);
+  int rc = at_level(c, level, &v);
+  return rc ? rc : from_view(c, v, fhe_rotate(v, ct, g, gk, out, n_ct));
+}
+int fhe_keyswitch_at(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
+                     uint32_t level) {
+  fhe_ctx *v;
+  DeviceBind bind(c);
+  int rc = at_level(c, level, &v);
+  return rc ? rc : from_view(c, v, fhe_keyswitch(v, d, ksk, out, n));
+}
+
+int fhe_rescale(fhe_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t level) {
+  if (!c) return FHE_ERR_INVALID;
+  if (c->params.scheme != FHE_SCHEME_CKKS) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rescale is CKKS only");
+  if (level < 2 || level > c->L) return fhe_fail(c, FHE_ERR_INVALID, "rescale needs 2 <= level <= L");
+  if (!n_ct) return FHE_OK;
+  if (!ct || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
+  const size_t N = c->n, in_w = (size_t)2 * level * N, out_w = (size_t)2 * (level - 1) * N;
+  const uint64_t *ce = ct + n_ct * in_w, *oe = out + n_ct * out_w;
+  if (!(oe <= ct || ce <= out)) return fhe_fail(c, FHE_ERR_INVALID, "rescale output overlaps its input");
+  DeviceBind bind(c);
+  fhe_ctx *up, *lo;
+  int rc = ctx_level(c, level, &up);
+  if (!rc) rc = ctx_level(c, level - 1, &lo);
+  if (rc) return rc;
+  for (uint32_t c0 = 0; c0 < n_ct; c0 += kCtChunk) {
+    const uint32_t m = std::min(kCtChunk, n_ct - c0);
+    if ((rc = rescale_impl(up, lo, ct + c0 * in_w, out + c0 * out_w, m))) return from_view(c, lo, rc);
   }
   return FHE_OK;
 }

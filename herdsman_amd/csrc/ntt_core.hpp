@@ -68,7 +68,10 @@
 #define CONV_T 1  // PRO_CONV target limbs per workgroup (conv_multi_body); 2 as first written spilled 34-98 VGPRs: headline 15.8k against 18.2k
 #endif
 #ifndef CONV_PIPE
-#define CONV_PIPE 1  // conv_multi_body: scheduling barriers between the prologue's source chunks
+#define CONV_PIPE 2  // conv_multi_body: source-load prefetch depth (elements)
+#endif
+#ifndef CONV_BUF
+#define CONV_BUF 0  // PRO_CONV (one target per workgroup): >0 buffer loads of the sources, that many elements ahead
 #endif
 #ifndef MODUP_COL_SPLIT
 #define MODUP_COL_SPLIT 1
@@ -110,6 +113,7 @@ struct NttArgs {
   // p = 2 ct + b, with ext [ct][e_ndig][e_QP][N] and ksk [e_ndig][2][e_QP][N]
   const u64 *e_ext, *e_ksk;
   u32 e_ndig, e_QP;
+  u32 e_kQP, e_kshift;  // key rows per digit half; key row of limb i >= L is i + e_kshift (level views)
   // PRO_TENSOR (first pass of the inverse NTT of d2 in CKKS mul+relin, poly =
   // ciphertext): the pass reads the operands a, b [ct][2][L][N] instead of d2,
   // writes the relinearisation base out[ct][0] = a0 b0, out[ct][1] = a0 b1 + a1 b0
@@ -728,6 +732,34 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       u32 hc0[NS], hc1[NS];  // the constants' 31-bit digits (uniform, SGPRs)
 #pragma unroll
       for (int i = 0; i < NS; ++i) split31(ep.h[i], hc0[i], hc1[i]);
+#if CONV_BUF
+      // buffer loads over the NS source limbs (one descriptor, 32-bit voffset,
+      // scalar soffset per (source, element)), CONV_BUF elements in flight; the
+      // loads of element r + PD carry a false dependence on element r - 1's
+      // result so the compiler cannot hoist them all (see conv_multi_body)
+      constexpr int PD = CONV_BUF;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void *)ep.src, 0, (u32)(NS * NW * 8), 0x00020000);
+      u32 voff_dep = voff;
+      u64 sv[PD + 1][NS];
+      const auto load_el = [&](u64(&d)[NS], int r) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b64(
+              rs, voff_dep, (u32)(i * NW * 8) + ((u32)GF::k_reg(r) << (PG::LS + 3)), 0);
+          d[i] = ((u64)v[1] << 32) | v[0];
+        }
+      };
+#pragma unroll
+      for (int r = 0; r < PD; ++r) load_el(sv[r], r);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r + PD < R) load_el(sv[(r + PD) % (PD + 1)], r + PD);
+        x[r] = CONV_COLS && SP && WIDE && CONV_SP60 ? dot_cols_sp60<NS>(sv[r % (PD + 1)], hc0, hc1, mi.q_hi)
+                                                    : dot_cols<NS, SP>(sv[r % (PD + 1)], hc0, hc1, mi);
+        asm volatile("" : "+v"(voff_dep) : "v"(x[r]));
+      }
+#else
 #pragma unroll
       for (int c0 = 0; c0 < R; c0 += 4) {
         u64 sv[4][NS];
@@ -742,6 +774,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
                       : CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                                  // < 2q
                                   : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);                   // < 4q
       }
+#endif
     } else {
       // the first forward pass may read out of place (NttArgs::src)
       const u64 *din = data;
@@ -790,35 +823,56 @@ __device__ __forceinline__ void conv_multi_body(const NttArgs &a, u64 *lds, u32 
 #pragma unroll
     for (int i = 0; i < NS; ++i) split31(a.c_h[(size_t)i * a.c_nd + act], hc0[t][i], hc1[t][i]);
   }
+  // group 0 of a forward column pass (stages 0-3, hi = 0, ts >> p = 0) uses the
+  // 15 twiddles tw[1..15] of its modulus in every thread: read them here, before
+  // any store, so they are scalar loads held in SGPRs for every target
+  static_assert(PG::S0 == 0 && Grp<S, LOGR, 0>::p == S - LOGR && (W << (S - LOGR)) <= (W << Grp<S, LOGR, 0>::p),
+                "group 0 twiddles are uniform");
+  u64 tz[CT][16];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const u32 act = t0 + ((u32)t < nt ? t : 0);
+    const u64 *twt = a.tw + ((size_t)(a.map.mod_offset + limbmap_limb(a.map, act)) << LOG_N);
+#pragma unroll
+    for (int k = 0; k < 15; ++k) tz[t][k] = twt[k + 1];
+    tz[t][15] = 0;
+  }
   const u64 *src = a.c_src + (((size_t)poly * a.c_src_stride + a.c_src_first) << LOG_N);
   const u32 voff_in = (gb + (GF::k_thr(ts) << PG::LS)) << 3;
   u64 x[CT][R];
-  // chunks of 4 elements (4 NS source words each), at most two chunks in
-  // flight: left alone the scheduler hoists all 16 NS loads (up to 226 VGPRs)
-  u64 sv[2][4][NS];
-  const auto load_chunk = [&](u64(&d)[4][NS], int c0) {
+  // the NS source words of element r + PD are in flight while element r's CT
+  // dot products run (PD + 1 element buffers of NS words): the whole 16-element
+  // prologue hoisted would need 2 NS R VGPRs on top of the CT R outputs
+  constexpr int PD = CONV_PIPE;
+  u64 sv[PD + 1][NS];
+  // element r of source i through ONE buffer descriptor over the NS source
+  // limbs: the per-thread part is the single 32-bit voffset, the (source,
+  // element) part a scalar soffset.  With global loads the compiler folds those
+  // offsets into 64-bit VGPR addresses (two VALU adds and two VGPRs per load)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, (u32)(NS * NW * 8), 0x00020000);
+  // The loads of element r + PD carry a false dependence on element r - 1's
+  // result (voff_dep): the source words are invariant loads, which the
+  // compiler otherwise hoists all at once (64 in flight for NS = 4, and the
+  // outputs spill)
+  u32 voff_dep = voff_in;
+  const auto load_el = [&](u64(&d)[NS], int r) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < NS; ++i) d[j][i] = ld_b(src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff_in);
+    for (int i = 0; i < NS; ++i) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(
+          rs, voff_dep, (u32)(i * NW * 8) + ((u32)GF::k_reg(r) << (PG::LS + 3)), 0);
+      d[i] = ((u64)v[1] << 32) | v[0];
+    }
   };
-  load_chunk(sv[0], 0);
 #pragma unroll
-  for (int k = 0; k < R / 4; ++k) {
-    if (k + 1 < R / 4) load_chunk(sv[(k + 1) & 1], 4 * (k + 1));
-#if CONV_PIPE
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+  for (int r = 0; r < PD; ++r) load_el(sv[r], r);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+  for (int r = 0; r < R; ++r) {
+    if (r + PD < R) load_el(sv[(r + PD) % (PD + 1)], r + PD);
 #pragma unroll
-      for (int t = 0; t < CT; ++t)
-        x[t][4 * k + j] = CONV_COLS && SP && WIDE && CONV_SP60
-                              ? dot_cols_sp60<NS>(sv[k & 1][j], hc0[t], hc1[t], q_hi[t])
-                              : dot_cols<NS, SP>(sv[k & 1][j], hc0[t], hc1[t], mt[t]);  // < 2q
-#if CONV_PIPE
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    for (int t = 0; t < CT; ++t)
+      x[t][r] = CONV_COLS && SP && WIDE && CONV_SP60 ? dot_cols_sp60<NS>(sv[r % (PD + 1)], hc0[t], hc1[t], q_hi[t])
+                                                     : dot_cols<NS, SP>(sv[r % (PD + 1)], hc0[t], hc1[t], mt[t]);  // < 2q
+    asm volatile("" : "+v"(voff_dep) : "v"(x[CT - 1][r]));
   }
   const u32 voff = (gb + (Grp<S, LOGR, NG - 1>::k_thr(ts) << PG::LS)) << 3;
   const EpiRow ep{};
@@ -830,10 +884,13 @@ __device__ __forceinline__ void conv_multi_body(const NttArgs &a, u64 *lds, u32 
     const u32 mod = a.map.mod_offset + limb;
     u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
     const u64 *tw = a.tw + ((size_t)mod << LOG_N);
-    u64 tc[16];
-    Grp<S, LOGR, 0>::template load_tw<PG::S0>(tc, tw, hi, ts);
+    u64(&tc)[16] = tz[t];
+#ifdef CONV_DIAG
+    for (int r = 0; r < R; ++r) st_b(data + ((size_t)r << PG::LS), voff, x[t][r] + tc[r]);
+#else
     group_loop<LOG_N, S, LOGR, W, false, true, SP, WIDE, EPI_NONE, 0>(x[t], tc, lds, tw, data, voff, w, ts, hi, a,
                                                                      mt[t], mod, ep);
+#endif
   }
 }
 
@@ -893,15 +950,19 @@ __global__ void __launch_bounds__(W << (S - LOGR),
     // L2 for the whole batch, and the b = 1 item re-reads the ext rows the
     // b = 0 item just fetched
     // GI groups are interleaved per XCD (their key rows all L2-resident)
+    // The remap is one-to-one only when the (limb, row block) groups fill the 8
+    // XCDs evenly; other shapes keep the plain blockIdx mapping
     constexpr u32 GIW = is_ksq(EPI) ? KSQ_GI : KSP_GI;
-    const u32 np = gridDim.y, lin = blockIdx.x + gridDim.x * (blockIdx.y + np * blockIdx.z);
-    const u32 r = lin >> 3, gpx = gridDim.x * gridDim.z / 8;  // groups per XCD
-    const u32 GI = gpx % GIW == 0 ? GIW : 1;
-    const u32 within = r % (GI * np);
-    const u32 g = ((r / (GI * np)) * GI + within % GI) * 8 + (lin & 7);  // g = (limb, row block)
-    poly = within / GI;
-    bx = g % gridDim.x;
-    act = g / gridDim.x;
+    if (((gridDim.x * gridDim.z) & 7) == 0) {
+      const u32 np = gridDim.y, lin = blockIdx.x + gridDim.x * (blockIdx.y + np * blockIdx.z);
+      const u32 r = lin >> 3, gpx = gridDim.x * gridDim.z / 8;  // groups per XCD
+      const u32 GI = gpx % GIW == 0 ? GIW : 1;
+      const u32 within = r % (GI * np);
+      const u32 g = ((r / (GI * np)) * GI + within % GI) * 8 + (lin & 7);  // g = (limb, row block)
+      poly = within / GI;
+      bx = g % gridDim.x;
+      act = g / gridDim.x;
+    }
   }
   if constexpr (is_conv(EPI)) {
     // the T target limbs of one source block (poly, column block) run on
@@ -951,19 +1012,20 @@ __global__ void __launch_bounds__(W << (S - LOGR),
 
   EpiRow ep{};
   if constexpr (is_ksp(EPI)) {
+    // P limbs: key row limb + e_kshift (a level view reads the full-level key)
     const size_t N = (size_t)1 << LOG_N;
     ep.ext_j = (size_t)a.e_QP * N;
-    ep.ksk_j = 2 * ep.ext_j;
+    ep.ksk_j = (size_t)2 * a.e_kQP * N;
     ep.kext = a.e_ext + ((size_t)(poly >> 1) * a.e_ndig * a.e_QP + limb) * N;
-    ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_QP + limb) * N;
+    ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_kQP + limb + a.e_kshift) * N;
   }
   if constexpr (is_combine(EPI)) {
     if constexpr (is_ksq(EPI)) {
       const size_t N = (size_t)1 << LOG_N;
       ep.ext_j = (size_t)a.e_QP * N;
-      ep.ksk_j = 2 * ep.ext_j;
+      ep.ksk_j = (size_t)2 * a.e_kQP * N;
       ep.kext = a.e_ext + ((size_t)(poly >> 1) * a.e_ndig * a.e_QP + limb) * N;
-      ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_QP + limb) * N;
+      ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_kQP + limb) * N;  // Q limbs: key row = limb
     }
     ep.acc = a.e_acc + (((size_t)poly * a.e_acc_stride + limb) << LOG_N);
     ep.base = a.e_base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);

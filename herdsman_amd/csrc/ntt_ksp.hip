@@ -83,6 +83,8 @@ int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32
     a.e_ksk = ksk;
     a.e_ndig = ndig;
     a.e_QP = QP;
+    a.e_kQP = ctx_key_qp(c);
+    a.e_kshift = c->key_pshift;
     const u32 n_jobs = np * K;
     int rc;
     switch (ndig) {

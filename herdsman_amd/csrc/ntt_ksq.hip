@@ -11,7 +11,7 @@
 // forms acc[2 ct + b][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1 itself.
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro, const u64 *ext, const u64 *ksk, u32 ndig,
-                           u32 base_g) {
+                           u32 base_g, const u64 *pinv) {
   const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
   if (ext && (c->log_n <= 14 || ndig > 4 || (n_polys & 1)))
@@ -29,7 +29,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
     a.e_acc = acc + (size_t)p0 * acc_stride * N;
     a.e_base = base + (size_t)p0 * L * N;
     a.e_out = out + (size_t)p0 * L * N;
-    a.e_pinv = c->d_pinv;
+    a.e_pinv = pinv ? pinv : c->d_pinv;
     a.e_acc_stride = acc_stride;
     a.e_add_mask = add_mask;
     a.e_g = base_g & ((2u << c->log_n) - 1);
@@ -38,6 +38,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
       a.e_ksk = ksk;
       a.e_ndig = ndig;
       a.e_QP = QP;
+      a.e_kQP = ctx_key_qp(c);
     }
     const u32 n_jobs = np * L;
     int rc;

@@ -202,7 +202,8 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_prep_kernel(const u64 *__restrict
 template <bool SP, int MAXD>
 __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restrict__ ext, const u64 *__restrict__ ksk,
                                                             u64 *__restrict__ acc, const ModInfo *mods, u32 QP,
-                                                            u32 ndig, u32 n_ct, u32 log_n, u32 limb0) {
+                                                            u32 ndig, u32 n_ct, u32 log_n, u32 limb0, u32 kQP,
+                                                            u32 L, u32 kshift) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 i = limb0 + blockIdx.y;
   const size_t N = (size_t)1 << log_n;
@@ -210,14 +211,16 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restric
   const size_t ext_ct = (size_t)ndig * QP * N, acc_ct = (size_t)2 * QP * N;
   const u64 *e = ext + (size_t)i * N + k;
   u64 *o = acc + (size_t)i * N + k;
-  const u64 *kp = ksk + (size_t)i * N + k;  // key word (j, b) at kp[(2 j + b) QP N]
+  // key word (j, b) at kp[(2 j + b) kQP N]; the key row of a P limb of a level
+  // view is i + kshift (the full-level key layout)
+  const u64 *kp = ksk + (size_t)(i + (i >= L ? kshift : 0)) * N + k;
   if constexpr (MAXD > 0) {
     // the 2 ndig key words of this coefficient stay in registers for the whole batch
     u64 k0[MAXD], k1[MAXD];
 #pragma unroll
     for (int j = 0; j < MAXD; ++j) {
-      k0[j] = j < (int)ndig ? kp[(size_t)(2 * j) * QP * N] : 0;
-      k1[j] = j < (int)ndig ? kp[(size_t)(2 * j + 1) * QP * N] : 0;
+      k0[j] = j < (int)ndig ? kp[(size_t)(2 * j) * kQP * N] : 0;
+      k1[j] = j < (int)ndig ? kp[(size_t)(2 * j + 1) * kQP * N] : 0;
     }
     // software pipeline over the batch: the next ciphertext's digit words are
     // in flight while this one's products are formed
@@ -247,8 +250,8 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_inner_kernel(const u64 *__restric
         for (int j = 0; j < 4; ++j) {
           const bool on = j < (int)nj;
           x[j] = on ? ld_nt(e + ct * ext_ct + (size_t)(j0 + j) * QP * N) : 0;
-          h0[j] = on ? kp[(size_t)(2 * (j0 + j)) * QP * N] : 0;
-          h1[j] = on ? kp[(size_t)(2 * (j0 + j) + 1) * QP * N] : 0;
+          h0[j] = on ? kp[(size_t)(2 * (j0 + j)) * kQP * N] : 0;
+          h1[j] = on ? kp[(size_t)(2 * (j0 + j) + 1) * kQP * N] : 0;
         }
         r0 = add_mod(r0, dot_mont<4, SP>(x, h0, 1, nj, m), m.q);
         r1 = add_mod(r1, dot_mont<4, SP>(x, h1, 1, nj, m), m.q);
@@ -452,6 +455,26 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   }
 }
 
+// CKKS rescale, the lift of the dropped limb (orc_rescale): x = INTT(c_{m})
+// in [0, q_m) becomes, for each remaining modulus q_i, [x]_{q_i} if
+// x <= q_m / 2, else [x - q_m]_{q_i} (the central lift OpenFHE's SwitchModulus
+// and SEAL's divide_and_round_q_last use).  x [2n][N] -> conv [2n][m][N],
+// canonical; the NTT of conv and the finish (c_i - NTT(conv)) q_m^-1 run in
+// ntt_fwd_combine_launch.
+template <bool SP>
+__global__ void __launch_bounds__(EW_BLOCK) rescale_lift_kernel(const u64 *__restrict__ x, u64 *__restrict__ conv,
+                                                                const ModInfo *mods, const u64 *qm_mod, u32 m,
+                                                                u64 half, u32 log_n) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 p = blockIdx.y / m, i = blockIdx.y % m;
+  const size_t N = (size_t)1 << log_n;
+  const ModInfo mi = mods[i];
+  const u64 v = x[(size_t)p * N + k];
+  u64 r = reduce128<SP>(U128{v, 0}, mi);  // exact v mod q_i
+  if (v > half) r = sub_mod(r, qm_mod[i], mi.q);
+  conv[((size_t)p * m + i) * N + k] = r;
+}
+
 // ------------------------------------------------------- host launchers
 template <bool SP>
 int ew_impl(fhe_ctx *c, EwOp op, const u64 *a, const u64 *b, u64 *out, u32 jobs, u32 mod_begin, u32 n_limbs) {
@@ -490,16 +513,16 @@ int modup_impl(fhe_ctx *c, const u64 *dc, u32 dcs, u64 *ext, u32 n, u32 ndig) {
 // limbs [limb0, limb0 + nl) of Q u P
 template <bool SP>
 int inner_impl(fhe_ctx *c, const u64 *ext, const u64 *ksk, u64 *acc, u32 n, u32 ndig, u32 limb0, u32 nl) {
-  const u32 QP = c->L + c->K;
+  const u32 QP = c->L + c->K, kQP = ctx_key_qp(c), L = c->L, ks = c->key_pshift;
   dim3 grid(c->n / EW_BLOCK, nl);
   if (ndig <= 4)
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 4>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 4>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0, kQP, L, ks);
   else if (ndig <= 8)
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 8>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 8>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0, kQP, L, ks);
   else if (ndig <= 16)
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 16>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 16>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0, kQP, L, ks);
   else
-    hipLaunchKernelGGL((ks_inner_kernel<SP, 0>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0);
+    hipLaunchKernelGGL((ks_inner_kernel<SP, 0>), grid, dim3(EW_BLOCK), 0, c->stream, ext, ksk, acc, c->d_mods, QP, ndig, n, c->log_n, limb0, kQP, L, ks);
   return fhe_check(c, hipGetLastError(), "ks_inner_kernel");
 }
 
@@ -739,6 +762,46 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
   return keyswitch_run(c, w, gk, base, out, n, 1u, ntt_form);
 }
 
+
+// ------------------------------------------------------------ CKKS rescale
+size_t rescale_ws_bytes(const fhe_ctx *lo, u32 n) { return sizeof(u64) * lo->n * 2 * (size_t)n * (1 + lo->L); }
+
+template <bool SP>
+static int rescale_lift(fhe_ctx *lo, const u64 *x, u64 *conv, const u64 *qm_mod, u64 half, u32 n_polys) {
+  const u32 m = lo->L, per = std::max<u32>(1, kMaxGridY / m);
+  for (u32 p0 = 0; p0 < n_polys; p0 += per) {
+    const u32 np = std::min(per, n_polys - p0);
+    hipLaunchKernelGGL((rescale_lift_kernel<SP>), dim3(lo->n / EW_BLOCK, np * m), dim3(EW_BLOCK), 0, lo->stream,
+                       x + (size_t)p0 * lo->n, conv + (size_t)p0 * m * lo->n, lo->d_mods, qm_mod, m, half,
+                       lo->log_n);
+    int rc = fhe_check(lo, hipGetLastError(), "rescale_lift_kernel");
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
+// Rescale n ciphertexts of level m + 1 (context `up`) to level m (context
+// `lo`): the dropped limb c_m of each of the 2n polys is copied out and
+// inverse-transformed over q_m on `up`, lifted to the m remaining moduli,
+// and ntt_fwd_combine_launch transforms the lift and forms
+// out_i = (c_i - NTT(lift)_i) q_m^-1 in its last pass (acc = ct with stride
+// m + 1 limbs, the epilogue constant d_qdrop = q_m^-1 R).
+int rescale_impl(fhe_ctx *up, fhe_ctx *lo, const u64 *ct, u64 *out, u32 n) {
+  const u32 m = lo->L;
+  const size_t N = lo->n;
+  void *ws;
+  int rc = ctx_workspace(lo, rescale_ws_bytes(lo, n), &ws);
+  if (rc) return rc;
+  u64 *x = (u64 *)ws, *conv = x + (size_t)2 * n * N;
+  if ((rc = fhe_check(lo, hipMemcpy2DAsync(x, N * 8, ct + (size_t)m * N, (size_t)(m + 1) * N * 8, N * 8, 2 * n,
+                                           hipMemcpyDeviceToDevice, lo->stream), "rescale copy")))
+    return rc;
+  if ((rc = ntt_launch(up, LimbMap{x, 1, 1, 0, 1, 0, m, 2 * n}, true))) return rc;
+  const u64 qm = up->moduli[m];
+  if ((rc = SP_DISPATCH(lo, rescale_lift, lo, x, conv, lo->d_qdrop + m, qm >> 1, 2 * n))) return rc;
+  return ntt_fwd_combine_launch(lo, conv, 2 * n, ct, m + 1, out, out, 0u, nullptr, nullptr, nullptr, 0, 0,
+                                lo->d_qdrop);
+}
 
 // ------------------------------------------------------------ BEHZ setup
 int behz_setup(fhe_ctx *c) {

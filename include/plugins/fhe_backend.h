@@ -137,6 +137,30 @@ int fhe_rotate(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const uint
 /* 5^steps mod 2N (steps may be negative); conjugation is 2N-1 */
 int fhe_galois_elt(const fhe_ctx *ctx, int32_t steps, uint32_t *out);
 
+/* ---- CKKS levels ("+ optional rescale") ---------------
+ * A CKKS ciphertext at level m (1 <= m <= L) holds the first m Q limbs:
+ * [n_ct][2][m][N], NTT form.  The *_at calls take such ciphertexts; key
+ * switching at level m uses the FULL-level keys ([dnum][2][L+K][N]), reading
+ * their rows of Q_m u P, with the digits partitioning the m active limbs by
+ * alpha = ceil(L/dnum) (the last digit possibly partial) -- OpenFHE's hybrid
+ * key switching at a reduced level (KeySwitchHYBRID on a level-dropped
+ * DCRTPoly), which herdsman's linked library performs per multiply
+ * (/root/reference/CMakeLists.txt:73,210-211).  level = L is the plain call.
+ * BFV contexts support only level = L (FHE_ERR_UNSUPPORTED otherwise). */
+int fhe_add_at(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct, uint32_t level);
+int fhe_sub_at(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct, uint32_t level);
+int fhe_mul_relin_at(fhe_ctx *ctx, const uint64_t *a, const uint64_t *b, const uint64_t *rlk, uint64_t *out,
+                     uint32_t n_ct, uint32_t level);
+int fhe_rotate_at(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const uint64_t *gk, uint64_t *out,
+                  uint32_t n_ct, uint32_t level);
+int fhe_keyswitch_at(fhe_ctx *ctx, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
+                     uint32_t level);
+/* CKKS rescale, level -> level - 1 (2 <= level <= L): out [n_ct][2][level-1][N]
+ * = round(ct / q_{level-1}) -- OpenFHE DCRTPoly::DropLastElementAndScale /
+ * SEAL divide_and_round_q_last_ntt (the dropped limb lifted centrally).
+ * out must not overlap ct. */
+int fhe_rescale(fhe_ctx *ctx, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t level);
+
 /* ---- reductions ---------------------------------------
  * Homomorphic reduction of n_ct ciphertexts to one, the evaluation of one
  * herdsman ReduceTask (the cross-partition tree itself is planned by

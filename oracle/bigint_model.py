@@ -215,10 +215,13 @@ class Params:
 
 
 # ------------------------------------------------------- hybrid keyswitch
-def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool):
-    """Hybrid key switching.  d: L limbs (NTT form if ntt_form).  ksk[j][b][i]
-    limb i of Q u P (NTT form).  Returns (ks0, ks1), each L limbs."""
-    L, K = p.L, p.K
+def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = None):
+    """Hybrid key switching at level lvl (default L).  d: lvl limbs (NTT form if
+    ntt_form).  ksk[j][b][i] limb i of Q u P of the FULL-level key (NTT form);
+    at a reduced level the digits partition the lvl active limbs by alpha and
+    only the key rows of Q_lvl u P are used.  Returns (ks0, ks1), each lvl limbs."""
+    L, K = (p.L if lvl is None else lvl), p.K
+    mi = list(range(L)) + [p.L + k for k in range(K)]  # level space -> modulus / key row
     QP = list(range(L + K))
     if ntt_form:
         dn, dc = d, p.intt(d, range(L))
@@ -230,8 +233,8 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool):
         if lo >= L:
             break
         others = [i for i in QP if not (lo <= i < hi)]
-        conv = base_conv(dc[lo:hi], p.moduli[lo:hi], [p.moduli[i] for i in others])
-        conv_n = p.ntt(conv, others)
+        conv = base_conv(dc[lo:hi], p.moduli[lo:hi], [p.moduli[mi[i]] for i in others])
+        conv_n = p.ntt(conv, [mi[i] for i in others])
         ext = {}
         for i in range(lo, hi):
             ext[i] = dn[i]
@@ -239,22 +242,23 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool):
             ext[i] = c
         for b in range(2):
             for i in QP:
-                q = p.moduli[i]
-                kb = ksk[j][b][i]
+                q = p.moduli[mi[i]]
+                kb = ksk[j][b][mi[i]]
                 e = ext[i]
                 row = acc[b][i]
                 for k in range(p.n):
                     row[k] = (row[k] + e[k] * kb[k]) % q
     Pprod = math.prod(p.P)
+    Qs = p.moduli[:L]
     out = []
     for b in range(2):
         if ntt_form:
-            accP = p.intt(acc[b][L:], range(L, L + K))
+            accP = p.intt(acc[b][L:], range(p.L, p.L + K))
             accQ = acc[b][:L]
         else:
-            allc = p.intt(acc[b], QP)
-            accP, accQ = allc[L:], allc[:L]
-        conv = base_conv(accP, p.P, p.Q)
+            accQ = p.intt(acc[b][:L], range(L))
+            accP = p.intt(acc[b][L:], range(p.L, p.L + K))
+        conv = base_conv(accP, p.P, Qs)
         if ntt_form:
             conv = p.ntt(conv, range(L))
         res = []
@@ -263,6 +267,43 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool):
             pinv = pow(Pprod % q, -1, q)
             res.append([(accQ[i][k] - conv[i][k]) * pinv % q for k in range(p.n)])
         out.append(res)
+    return out
+
+
+def ckks_mul_relin_at(p: Params, a, b, rlk, lvl: int):
+    """ckks_mul_relin on ciphertexts of lvl limbs (the first lvl Q primes)."""
+    n = p.n
+    d0, d1, d2 = [], [], []
+    for i in range(lvl):
+        q = p.moduli[i]
+        d0.append([a[0][i][k] * b[0][i][k] % q for k in range(n)])
+        d1.append([(a[0][i][k] * b[1][i][k] + a[1][i][k] * b[0][i][k]) % q for k in range(n)])
+        d2.append([a[1][i][k] * b[1][i][k] % q for k in range(n)])
+    ks0, ks1 = keyswitch(p, d2, rlk, True, lvl)
+    return [[[(x + y) % p.moduli[i] for x, y in zip(d0[i], ks0[i])] for i in range(lvl)],
+            [[(x + y) % p.moduli[i] for x, y in zip(d1[i], ks1[i])] for i in range(lvl)]]
+
+
+def rescale(p: Params, ct, lvl: int):
+    """CKKS rescale of an NTT-form ciphertext of lvl limbs, by its definition on
+    integers: each coefficient c in [0, Q_lvl) (CRT) becomes round(c / q_{lvl-1})
+    = (c - r) / q_{lvl-1} with r the centred residue of c mod q_{lvl-1} (ties,
+    r = (q-1)/2, round down as in OpenFHE / SEAL), reduced mod the remaining
+    lvl - 1 primes and transformed back."""
+    Qs, ql = p.moduli[:lvl], p.moduli[lvl - 1]
+    out = []
+    for poly in ct:
+        coef = p.intt(poly, range(lvl))
+        res = [[0] * p.n for _ in range(lvl - 1)]
+        for k in range(p.n):
+            c = crt([coef[i][k] for i in range(lvl)], Qs)
+            r = c % ql
+            if r > ql // 2:
+                r -= ql
+            v = (c - r) // ql
+            for i in range(lvl - 1):
+                res[i][k] = v % Qs[i]
+        out.append(p.ntt(res, range(lvl - 1)))
     return out
 
 

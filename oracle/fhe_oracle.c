@@ -384,10 +384,19 @@ void orc_base_conv(const orc_ctx *c, const uint64_t *src, const uint32_t *src_mo
 }
 
 /* --------------------------------------------------------- key switching */
-/* Hybrid key switching (dnum digits of alpha limbs, K special primes).
+/* Hybrid key switching (dnum digits of alpha limbs, K special primes) at level
+ * lvl <= L: d has the lvl active Q limbs, the digits partition them by alpha
+ * (the last digit may be partial, digits past lvl are empty), ModUp extends
+ * each digit to Q_lvl u P and the inner product uses the key rows of those
+ * moduli: Q rows 0..lvl-1 and P rows L..L+K-1 of the full-level key (the
+ * gadget g_j is P on digit j's limbs and 0 elsewhere, so dropping limbs keeps
+ * sum_j [d]_{Q_j} g_j = P d mod q_i; OpenFHE's KeySwitchHYBRID at a reduced
+ * level).  Level space: index i < lvl is q_i, lvl + k is p_k (modulus L + k).
  * in_ntt: 1 if d (and the result) is in NTT form (CKKS), 0 for coef form (BFV). */
-static void keyswitch_one(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, int in_ntt) {
-  const uint32_t n = c->n, L = c->L, K = c->K, QP = L + K, A = c->alpha;
+static void keyswitch_lvl(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, int in_ntt,
+                          uint32_t lvl) {
+  const uint32_t n = c->n, L = lvl, K = c->K, QP = L + K, QPk = c->L + K, A = c->alpha;
+#define MI(i) ((i) < L ? (i) : c->L + ((i) - L))
   uint64_t *dc = malloc(sizeof(uint64_t) * L * n);        /* d in coef form */
   uint64_t *dn = malloc(sizeof(uint64_t) * L * n);        /* d in NTT form */
   uint64_t *ext = malloc(sizeof(uint64_t) * QP * n);
@@ -405,34 +414,35 @@ static void keyswitch_one(const orc_ctx *c, const uint64_t *d, const uint64_t *k
     for (uint32_t i = lo; i < hi; ++i) { sq[i - lo] = c->m[i].q; sp[i - lo] = dc + (size_t)i * n; }
     for (uint32_t i = 0; i < QP; ++i) {
       if (i >= lo && i < hi) { memcpy(ext + (size_t)i * n, dn + (size_t)i * n, sizeof(uint64_t) * n); continue; }
-      dq[nd] = c->m[i].q; didx[nd] = i; dp[nd] = ext + (size_t)i * n; ++nd;
+      dq[nd] = c->m[MI(i)].q; didx[nd] = i; dp[nd] = ext + (size_t)i * n; ++nd;
     }
     conv_tab_init(T, sq, hi - lo, dq, nd);
     conv_apply(T, sp, dp, n);
-    for (uint32_t k = 0; k < nd; ++k) ntt_fwd_limb(&c->m[didx[k]], ext + (size_t)didx[k] * n, n);
-    /* inner product with key digit j */
+    for (uint32_t k = 0; k < nd; ++k) ntt_fwd_limb(&c->m[MI(didx[k])], ext + (size_t)didx[k] * n, n);
+    /* inner product with key digit j (its rows of Q_lvl u P) */
     for (uint32_t b = 0; b < 2; ++b) {
-      const uint64_t *kj = ksk + ((size_t)(j * 2 + b) * QP) * n;
+      const uint64_t *kj = ksk + ((size_t)(j * 2 + b) * QPk) * n;
       uint64_t *ab = acc + (size_t)b * QP * n;
       for (uint32_t i = 0; i < QP; ++i) {
-        const uint64_t q = c->m[i].q;
+        const uint64_t q = c->m[MI(i)].q;
+        const uint64_t *kr = kj + (size_t)MI(i) * n;
         for (uint32_t k = 0; k < n; ++k) {
           size_t o = (size_t)i * n + k;
-          ab[o] = addmod(ab[o], mulmod(ext[o], kj[o], q), q);
+          ab[o] = addmod(ab[o], mulmod(ext[o], kr[k], q), q);
         }
       }
     }
   }
   /* ModDown: (acc_Q - Conv_{P->Q}(acc_P)) * P^-1 */
   uint64_t pq[MAXM], qq[MAXM];
-  for (uint32_t k = 0; k < K; ++k) pq[k] = c->m[L + k].q;
+  for (uint32_t k = 0; k < K; ++k) pq[k] = c->m[c->L + k].q;
   for (uint32_t i = 0; i < L; ++i) qq[i] = c->m[i].q;
   conv_tab_init(T, pq, K, qq, L);
   uint64_t *conv = malloc(sizeof(uint64_t) * L * n);
   for (uint32_t b = 0; b < 2; ++b) {
     uint64_t *ab = acc + (size_t)b * QP * n;
-    if (in_ntt) orc_ntt_inv(c, ab + (size_t)L * n, 1, L, K);
-    else orc_ntt_inv(c, ab, 1, 0, QP);
+    if (!in_ntt) orc_ntt_inv(c, ab, 1, 0, L);
+    orc_ntt_inv(c, ab + (size_t)L * n, 1, c->L, K);
     const uint64_t *sp[MAXM]; uint64_t *dp[MAXM];
     for (uint32_t k = 0; k < K; ++k) sp[k] = ab + (size_t)(L + k) * n;
     for (uint32_t i = 0; i < L; ++i) dp[i] = conv + (size_t)i * n;
@@ -450,7 +460,12 @@ static void keyswitch_one(const orc_ctx *c, const uint64_t *d, const uint64_t *k
       }
     }
   }
+#undef MI
   free(conv); free(T); free(dc); free(dn); free(ext); free(acc);
+}
+
+static void keyswitch_one(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, int in_ntt) {
+  keyswitch_lvl(c, d, ksk, out, in_ntt, c->L);
 }
 
 void orc_keyswitch(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n) {
@@ -633,8 +648,8 @@ static void bfv_mul_relin_one(const orc_ctx *c, const behz_tab *B, const uint64_
 }
 
 static void ckks_mul_relin_one(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
-                               uint64_t *out) {
-  const size_t L = c->L, N = c->n;
+                               uint64_t *out, uint32_t lvl) {
+  const size_t L = lvl, N = c->n;
   uint64_t *d = malloc(sizeof(uint64_t) * 3 * L * N);
   uint64_t *ks = malloc(sizeof(uint64_t) * 2 * L * N);
   const uint64_t *a0 = a, *a1 = a0 + L * N, *b0 = b, *b1 = b0 + L * N;
@@ -647,7 +662,7 @@ static void ckks_mul_relin_one(const orc_ctx *c, const uint64_t *a, const uint64
       d[2 * L * N + o] = mulmod(a1[o], b1[o], q);
     }
   }
-  keyswitch_one(c, d + 2 * L * N, rlk, ks, 1);
+  keyswitch_lvl(c, d + 2 * L * N, rlk, ks, 1, lvl);
   orc_add(c, d, ks, out, 2, 0, (uint32_t)L);
   free(d); free(ks);
 }
@@ -665,23 +680,73 @@ void orc_mul_relin(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const
 #pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
   for (long i = 0; i < (long)n_ct; ++i) {
     if (B) bfv_mul_relin_one(c, B, a + i * CT, b + i * CT, rlk, out + i * CT);
-    else ckks_mul_relin_one(c, a + i * CT, b + i * CT, rlk, out + i * CT);
+    else ckks_mul_relin_one(c, a + i * CT, b + i * CT, rlk, out + i * CT, c->L);
   }
   free(B);
 }
 
-void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
-                uint32_t n_ct) {
-  const size_t L = c->L, N = c->n, CT = 2 * L * N;
+static void rotate_lvl(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
+                       uint32_t n_ct, uint32_t lvl) {
+  const size_t L = lvl, N = c->n, CT = 2 * L * N;
   uint64_t *tmp = malloc(sizeof(uint64_t) * CT), *ks = malloc(sizeof(uint64_t) * CT);
   for (uint32_t i = 0; i < n_ct; ++i) {
     if (c->scheme == ORC_SCHEME_CKKS) orc_automorph_ntt(c, ct + i * CT, tmp, g, 2, (uint32_t)L);
     else orc_automorph_coef(c, ct + i * CT, tmp, g, 2, 0, (uint32_t)L);
-    keyswitch_one(c, tmp + L * N, gk, ks, c->scheme == ORC_SCHEME_CKKS);
+    keyswitch_lvl(c, tmp + L * N, gk, ks, c->scheme == ORC_SCHEME_CKKS, lvl);
     orc_add(c, tmp, ks, out + i * CT, 1, 0, (uint32_t)L);
     memcpy(out + i * CT + L * N, ks + L * N, sizeof(uint64_t) * L * N);
   }
   free(tmp); free(ks);
+}
+
+void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
+                uint32_t n_ct) {
+  rotate_lvl(c, ct, g, gk, out, n_ct, c->L);
+}
+
+/* ------------------------------------------------- CKKS levels (rescale) */
+void orc_keyswitch_at(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
+                      uint32_t lvl) {
+  const size_t N = c->n;
+  for (uint32_t i = 0; i < n; ++i)
+    keyswitch_lvl(c, d + i * lvl * N, ksk, out + i * 2 * lvl * N, c->scheme == ORC_SCHEME_CKKS, lvl);
+}
+
+void orc_mul_relin_at(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
+                      uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+  const size_t CT = 2 * (size_t)lvl * c->n;
+#pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
+  for (long i = 0; i < (long)n_ct; ++i) ckks_mul_relin_one(c, a + i * CT, b + i * CT, rlk, out + i * CT, lvl);
+}
+
+void orc_rotate_at(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
+                   uint32_t n_ct, uint32_t lvl) {
+  rotate_lvl(c, ct, g, gk, out, n_ct, lvl);
+}
+
+/* CKKS rescale (OpenFHE DCRTPoly::DropLastElementAndScale, SEAL
+ * divide_and_round_q_last_ntt_inplace): for the last limb x = INTT(c_{l-1})
+ * lifted centrally (x - q_{l-1} if x > q_{l-1}/2, the same value both
+ * libraries use), out_i = (c_i - NTT_i([x]_{q_i})) * q_{l-1}^-1 mod q_i,
+ * i < l - 1 -- round(c / q_{l-1}) in RNS. */
+void orc_rescale(const orc_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+  const size_t N = c->n, Li = lvl, Lo = lvl - 1;
+  const uint64_t ql = c->m[Lo].q, half = ql >> 1;
+#pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
+  for (long e = 0; e < 2 * (long)n_ct; ++e) {
+    const uint64_t *src = ct + (size_t)e * Li * N;
+    uint64_t *dst = out + (size_t)e * Lo * N;
+    uint64_t *x = malloc(sizeof(uint64_t) * N), *y = malloc(sizeof(uint64_t) * N);
+    memcpy(x, src + Lo * N, sizeof(uint64_t) * N);
+    ntt_inv_limb(&c->m[Lo], x, (uint32_t)N);
+    for (uint32_t i = 0; i < Lo; ++i) {
+      const uint64_t q = c->m[i].q, qlm = ql % q, qinv = invmod(qlm, q);
+      for (size_t k = 0; k < N; ++k) y[k] = x[k] > half ? submod(x[k] % q, qlm, q) : x[k] % q;
+      ntt_fwd_limb(&c->m[i], y, (uint32_t)N);
+      for (size_t k = 0; k < N; ++k) dst[i * N + k] = mulmod(submod(src[i * N + k], y[k], q), qinv, q);
+    }
+    free(x); free(y);
+  }
 }
 
 /* -------------------------------------------------------------- sampling */

@@ -86,6 +86,18 @@ void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t galois, const uin
                 uint64_t *out, uint32_t n_ct);
 uint32_t orc_galois_elt(const orc_ctx *c, int32_t steps);
 
+/* ---- CKKS levels: ciphertexts [n_ct][2][lvl][N] with the first lvl Q primes
+ * (1 <= lvl <= L).  Key switching at level lvl uses the full-level key's rows
+ * of Q_lvl u P (digits partition the lvl limbs by alpha). */
+void orc_keyswitch_at(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
+                      uint32_t lvl);
+void orc_mul_relin_at(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
+                      uint64_t *out, uint32_t n_ct, uint32_t lvl);
+void orc_rotate_at(const orc_ctx *c, const uint64_t *ct, uint32_t galois, const uint64_t *gk,
+                   uint64_t *out, uint32_t n_ct, uint32_t lvl);
+/* rescale level lvl -> lvl - 1 (lvl >= 2): out [n_ct][2][lvl-1][N] = round(ct / q_{lvl-1}) */
+void orc_rescale(const orc_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t lvl);
+
 /* ---- test helpers: sampling, keys, encryption */
 void orc_fill_uniform(const orc_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin,
                       uint32_t n_limbs, uint64_t seed);

@@ -102,14 +102,49 @@ def gen_bfv(rng):
              out_mul=arr(out_mul), out_add=arr(out_add), g=np.uint32(g), out_rot=arr(out_rot))
 
 
+def gen_ckks_levels(rng):
+    """CKKS at reduced levels: L = 5 primes, alpha = 3 (dnum 2), so level 4 has
+    a partial second digit, level 3 one full digit and level 2 one partial
+    digit; mul+relin / rotate with the full-level key's Q_lvl u P rows, and the
+    rescale chain 5 -> 4 -> 3 by its integer definition."""
+    log_n, L, K, dnum = 10, 5, 2, 2
+    n = 1 << log_n
+    Q = M.gen_primes(60, log_n, L)
+    P = M.gen_primes(61, log_n, K, exclude=Q)
+    p = M.Params(log_n, L, K, dnum, Q + P, "ckks")
+    rlk = [[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(dnum)]
+    res = {}
+    for lvl in (4, 2):
+        a = [rand_limbs(rng, Q[:lvl], n) for _ in range(2)]
+        b = [rand_limbs(rng, Q[:lvl], n) for _ in range(2)]
+        res[f"a{lvl}"], res[f"b{lvl}"] = arr(a), arr(b)
+        res[f"mul{lvl}"] = arr(M.ckks_mul_relin_at(p, a, b, rlk, lvl))
+    a3 = [rand_limbs(rng, Q[:3], n) for _ in range(2)]
+    g = M.galois_elt(log_n, 5)
+    c0 = [M.automorph_ntt(x, g) for x in a3[0]]
+    c1 = [M.automorph_ntt(x, g) for x in a3[1]]
+    ks0, ks1 = M.keyswitch(p, c1, rlk, True, 3)
+    res["a3"], res["rot3"] = arr(a3), arr([[[(x + y) % Q[i] for x, y in zip(c0[i], ks0[i])] for i in range(3)], ks1])
+    c5 = [rand_limbs(rng, Q, n) for _ in range(2)]
+    r4 = M.rescale(p, c5, 5)
+    r3 = M.rescale(p, r4, 4)
+    res["c5"], res["r4"], res["r3"] = arr(c5), arr(r4), arr(r3)
+    np.savez(os.path.join(HERE, "ckks_levels_n1024_l5.npz"), log_n=np.uint32(log_n), L=np.uint32(L),
+             K=np.uint32(K), dnum=np.uint32(dnum), moduli=arr(Q + P), rlk=arr(rlk), g=np.uint32(g), **res)
+
+
 def main():
     rng = random.Random(0x48455244)
     gen_ntt(rng)
     gen_conv(rng)
     gen_ckks(rng)
     gen_bfv(rng)
+    gen_ckks_levels(random.Random(0x4C564C53))
     print("golden vectors written to", HERE)
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["levels"]:  # only the level fixture (the others are unchanged)
+        gen_ckks_levels(random.Random(0x4C564C53))
+    else:
+        main()

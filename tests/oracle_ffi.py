@@ -58,6 +58,10 @@ def lib():
         "orc_mul_relin": (None, [vp, _u64p, _u64p, _u64p, _u64p, u32]),
         "orc_rotate": (None, [vp, _u64p, u32, _u64p, _u64p, u32]),
         "orc_galois_elt": (u32, [vp, i32]),
+        "orc_keyswitch_at": (None, [vp, _u64p, _u64p, _u64p, u32, u32]),
+        "orc_mul_relin_at": (None, [vp, _u64p, _u64p, _u64p, _u64p, u32, u32]),
+        "orc_rotate_at": (None, [vp, _u64p, u32, _u64p, _u64p, u32, u32]),
+        "orc_rescale": (None, [vp, _u64p, _u64p, u32, u32]),
         "orc_fill_uniform": (None, [vp, _u64p, u32, u32, u32, u64]),
         "orc_sample_ternary": (None, [vp, u64, _i64p]),
         "orc_sample_cbd": (None, [vp, u64, _i64p]),
@@ -137,6 +141,28 @@ class Oracle:
     def keyswitch(self, d, ksk):
         out = np.zeros((d.shape[0], 2, self.L, self.n), dtype=np.uint64)
         self.lib.orc_keyswitch(self.h, np.ascontiguousarray(d), np.ascontiguousarray(ksk), out, d.shape[0])
+        return out
+
+    # ---- CKKS levels: ciphertexts [n][2][lvl][N] over the first lvl Q primes
+    def mul_relin_at(self, a, b, rlk, lvl):
+        out = np.zeros_like(a)
+        self.lib.orc_mul_relin_at(self.h, np.ascontiguousarray(a), np.ascontiguousarray(b),
+                                  np.ascontiguousarray(rlk), out, a.shape[0], lvl)
+        return out
+
+    def rotate_at(self, ct, g, gk, lvl):
+        out = np.zeros_like(ct)
+        self.lib.orc_rotate_at(self.h, np.ascontiguousarray(ct), g, np.ascontiguousarray(gk), out, ct.shape[0], lvl)
+        return out
+
+    def keyswitch_at(self, d, ksk, lvl):
+        out = np.zeros((d.shape[0], 2, lvl, self.n), dtype=np.uint64)
+        self.lib.orc_keyswitch_at(self.h, np.ascontiguousarray(d), np.ascontiguousarray(ksk), out, d.shape[0], lvl)
+        return out
+
+    def rescale(self, ct, lvl):
+        out = np.zeros((ct.shape[0], 2, lvl - 1, self.n), dtype=np.uint64)
+        self.lib.orc_rescale(self.h, np.ascontiguousarray(ct), out, ct.shape[0], lvl)
         return out
 
     def ct_add(self, a, b):

@@ -83,3 +83,39 @@ def test_bfv_rotate_golden():
     g, o = _bfv()
     out = o.rotate(g["a"][None], int(g["g"]), g["rlk"])
     assert np.array_equal(out[0], g["out_rot"])
+
+
+def _levels():
+    g = load("ckks_levels_n1024_l5.npz")
+    o = Oracle(SCHEME_CKKS, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), moduli=g["moduli"])
+    return g, o
+
+
+def test_ckks_level_mul_relin_golden():
+    """mul+relin at levels 4 (partial second digit) and 2 (one partial digit)
+    with the full-level key's Q_lvl u P rows (oracle/bigint_model.py keyswitch(lvl))."""
+    g, o = _levels()
+    for lvl in (4, 2):
+        out = o.mul_relin_at(g[f"a{lvl}"][None], g[f"b{lvl}"][None], g["rlk"], lvl)
+        assert np.array_equal(out[0], g[f"mul{lvl}"]), lvl
+
+
+def test_ckks_level_rotate_golden():
+    g, o = _levels()
+    out = o.rotate_at(g["a3"][None], int(g["g"]), g["rlk"], 3)
+    assert np.array_equal(out[0], g["rot3"])
+
+
+def test_ckks_rescale_golden():
+    """The RNS rescale equals round(c / q_last) on CRT-reconstructed integers."""
+    g, o = _levels()
+    r4 = o.rescale(g["c5"][None], 5)
+    assert np.array_equal(r4[0], g["r4"])
+    assert np.array_equal(o.rescale(r4, 4)[0], g["r3"])
+
+
+def test_full_level_calls_match_level_calls():
+    g, o = _ckks()
+    L = int(g["L"])
+    assert np.array_equal(o.mul_relin_at(g["a"][None], g["b"][None], g["rlk"], L),
+                          o.mul_relin(g["a"][None], g["b"][None], g["rlk"]))

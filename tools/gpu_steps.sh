@@ -8,6 +8,8 @@
 #   bench          the default bench.py line (CPU baseline and secondaries included)
 #   quick          bench.py --no-cpu --no-secondary --steps 3 --warmup 1
 #   ab=V1,V2,...   tools/ab_quick.sh over library variants ("main" = herdsman_amd/lib)
+#   abk=V1,V2,...  per-kernel A/B: rocprofv3 --kernel-trace --stats of op_bench ckks_mul per variant,
+#                  2 reps interleaved, then tools/kstat_cmp.py (op rate in each variant's log)
 #   stats          rocprofv3 --kernel-trace --stats of a short bench.py (roofline summary)
 #   steptable      rocprofv3 kernel trace of one C5 wave loop -> tools/step_table.py
 set -e
@@ -23,6 +25,20 @@ for s in "$@"; do
     bench) timeout -k 10 600 python3 bench.py > "$O/bench.log" 2>&1 ;;
     quick) timeout -k 10 300 python3 bench.py --no-cpu --no-secondary --steps 3 --warmup 1 > "$O/quick.log" 2>&1 ;;
     ab=*) IFS=, read -r -a vs <<< "${s#ab=}"; bash tools/ab_quick.sh "$O/q" "${vs[@]}" > "$O/ab.txt" 2>&1 ;;
+    abk=*) IFS=, read -r -a vs <<< "${s#abk=}"
+      lib_of() { if [ "$1" = main ]; then echo herdsman_amd/lib/libherdsman_fhe.so; else echo herdsman_amd/var/$1/libherdsman_fhe.so; fi; }
+      for v in "${vs[@]}"; do  # parity first: the digests and the metric-config parity cases
+        HERD_FHE_LIB=$(lib_of $v) timeout -k 10 300 python3 -u -m pytest tests/test_digests.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > "$O/parity.$v.log" 2>&1
+        echo "$v parity: $(tail -n 1 "$O/parity.$v.log")"
+      done
+      for v in "${vs[@]}"; do
+        HERD_FHE_LIB=$(lib_of $v) timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/k/$v" -o run -- python3 tools/op_bench.py ckks_mul --batch 128 --reps 5 > "$O/k.$v.log" 2>&1
+        f=$(find "$O/k/$v" -name run_kernel_stats.csv | head -n 1); cp "$f" "$O/k/$v/run_kernel_stats.csv" 2>/dev/null || true
+      done
+      python3 tools/kstat_cmp.py "$O/k" "${vs[@]}" > "$O/kcmp.txt"
+      for rep in 1 2 3; do for v in "${vs[@]}"; do
+        echo "$v rep$rep $(HERD_FHE_LIB=$(lib_of $v) timeout -k 10 200 python3 tools/op_bench.py ckks_mul --batch 128 --reps 20 2>/dev/null | tail -n 1)"
+      done; done > "$O/abk.txt" ;;
     stats) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/stats" -o run -- python3 bench.py --no-cpu --no-secondary --steps 3 --warmup 1 > "$O/stats.log" 2>&1 ;;
     steptable) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/step" -o run -- python3 tools/op_bench.py ckks_mul --batch 128 --reps 8 > "$O/step.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
