@@ -401,6 +401,131 @@ def bfv_mul_relin(p: Params, a, b, rlk):
             [[(x + y) % Q[i] for x, y in zip(res[1][i], ks1[i])] for i in range(L)]]
 
 
+# ------------------------------------------------------------- BFV HPS
+def hps_tables(p: Params):
+    """Constants of the HPS multiplication (Halevi-Polyakov-Shoup 2018; OpenFHE
+    BFVrns multiplication technique HPS) with P = the Bsk primes.  The doubles
+    are formed exactly as the C oracle and the backend form them:
+    (double)num / (double)q and 1.0 / (double)q, each a correctly rounded
+    IEEE-754 operation."""
+    Q, P, t = p.Q, p.Bsk, p.t
+    Qp, Pp = math.prod(Q), math.prod(P)
+    T = {"Q": Q, "P": P, "Qp": Qp, "Pp": Pp}
+    T["qt"] = [pow((Qp // q) % q, -1, q) for q in Q]                      # (Q/q_i)^-1 mod q_i
+    T["invq"] = [1.0 / float(q) for q in Q]
+    T["qstar_p"] = [[(Qp // q) % pj for pj in P] for q in Q]              # Q/q_i mod p_j
+    T["Q_p"] = [Qp % pj for pj in P]
+    num = [t * qt % q for qt, q in zip(T["qt"], Q)]                        # t (Q/q_i)^-1 mod q_i
+    T["frac"] = [float(nm) / float(q) for nm, q in zip(num, Q)]           # frac(t P c_i / q_i)
+    T["I"] = [[(-nm * pow(q, -1, pj)) % pj for pj in P] for nm, q in zip(num, Q)]
+    T["lam"] = [t * pow(Qp % pj, -1, pj) % pj for pj in P]                # t Q^-1 mod p_j
+    T["pt"] = [pow((Pp // pj) % pj, -1, pj) for pj in P]
+    T["invp"] = [1.0 / float(pj) for pj in P]
+    T["pstar_q"] = [[(Pp // pj) % q for q in Q] for pj in P]
+    T["P_q"] = [Pp % q for q in Q]
+    return T
+
+
+def hps_extend(T, xq):
+    """Q -> P exact base extension of the centred lift (HPS section 2.4): y_i =
+    [x_i (Q/q_i)^-1]_{q_i}, v = floor(0.5 + sum_i y_i / q_i) in doubles, and
+    x mod p_j = sum_i y_i [Q/q_i]_{p_j} - v [Q]_{p_j}."""
+    Q, P = T["Q"], T["P"]
+    n = len(xq[0])
+    out = [[0] * n for _ in P]
+    for k in range(n):
+        y = [xq[i][k] * T["qt"][i] % q for i, q in enumerate(Q)]
+        sm = 0.0
+        for i in range(len(Q)):
+            sm = sm + float(y[i]) * T["invq"][i]
+        v = int(sm + 0.5)
+        for j, pj in enumerate(P):
+            out[j][k] = (sum(y[i] * T["qstar_p"][i][j] for i in range(len(Q))) - v * T["Q_p"][j]) % pj
+    return out
+
+
+def hps_scale(T, eq, ep):
+    """round(t d / Q) for d given in Q u P (coefficient form, canonical), in P
+    (HPS simple scaling: integer parts I_ij, fractional parts in doubles), then
+    P -> Q by the exact extension of the centred lift."""
+    Q, P = T["Q"], T["P"]
+    n = len(eq[0])
+    out = [[0] * n for _ in Q]
+    for k in range(n):
+        nu = 0.5
+        for i in range(len(Q)):
+            nu = nu + float(eq[i][k]) * T["frac"][i]
+        r = int(nu)
+        z = [(sum(eq[i][k] * T["I"][i][j] for i in range(len(Q))) + r + ep[j][k] * T["lam"][j]) % pj
+             for j, pj in enumerate(P)]
+        y = [z[j] * T["pt"][j] % pj for j, pj in enumerate(P)]
+        sm = 0.0
+        for j in range(len(P)):
+            sm = sm + float(y[j]) * T["invp"][j]
+        v = int(sm + 0.5)
+        for i, q in enumerate(Q):
+            out[i][k] = (sum(y[j] * T["pstar_q"][j][i] for j in range(len(P))) - v * T["P_q"][i]) % q
+    return out
+
+
+def bfv_mul_relin_hps(p: Params, a, b, rlk, check_exact: bool = True):
+    """HPS multiplication + hybrid relinearization.  a, b: [2][L][N] coefficient
+    form.  With check_exact, each tensor output is compared with its definition
+    round(t d / Q) on integers (d the negacyclic tensor of the centred lifts):
+    the floating-point parts may differ from it by a few units, BFV noise."""
+    L, n, t = p.L, p.n, p.t
+    T = hps_tables(p)
+    Q, P = T["Q"], T["P"]
+    pmods = list(range(L + p.K, L + p.K + len(P)))
+    polys = [a[0], a[1], b[0], b[1]]
+    xq = [p.ntt(x, range(L)) for x in polys]
+    xp = [p.ntt(hps_extend(T, x), pmods) for x in polys]
+
+    def tensor(x, mods):
+        e0, e1, e2 = [], [], []
+        for i, m in enumerate(mods):
+            q = p.moduli[m]
+            a0, a1, b0, b1 = x[0][i], x[1][i], x[2][i], x[3][i]
+            e0.append([u * v % q for u, v in zip(a0, b0)])
+            e1.append([(u * v + w * z) % q for u, v, w, z in zip(a0, b1, a1, b0)])
+            e2.append([u * v % q for u, v in zip(a1, b1)])
+        return [e0, e1, e2]
+
+    eq = [p.intt(e, range(L)) for e in tensor(xq, range(L))]
+    ep = [p.intt(e, pmods) for e in tensor(xp, pmods)]
+    res = [hps_scale(T, e_q, e_p) for e_q, e_p in zip(eq, ep)]
+    if check_exact:
+        Qp = T["Qp"]
+        lift = [[_centered(crt([x[i][k] for i in range(L)], Q), Qp) for k in range(n)] for x in polys]
+        d = [negacyclic_int_poly(lift[0], lift[2]),
+             [u + v for u, v in zip(negacyclic_int_poly(lift[0], lift[3]), negacyclic_int_poly(lift[1], lift[2]))],
+             negacyclic_int_poly(lift[1], lift[3])]
+        for e, dd in zip(res, d):
+            for k in range(n):
+                want = (2 * t * dd[k] + Qp) // (2 * Qp)  # round(t d / Q), compared mod Q
+                got = crt([e[i][k] for i in range(L)], Q)
+                assert abs(_centered((got - want) % Qp, Qp)) <= 1 << 16, k
+    ks0, ks1 = keyswitch(p, res[2], rlk, False)
+    return [[[(x + y) % Q[i] for x, y in zip(res[0][i], ks0[i])] for i in range(L)],
+            [[(x + y) % Q[i] for x, y in zip(res[1][i], ks1[i])] for i in range(L)]]
+
+
+def negacyclic_int_poly(a: Sequence[int], b: Sequence[int]) -> List[int]:
+    """Exact negacyclic product over the integers (schoolbook)."""
+    n = len(a)
+    out = [0] * n
+    for i, ai in enumerate(a):
+        if ai == 0:
+            continue
+        for j, bj in enumerate(b):
+            k = i + j
+            if k < n:
+                out[k] += ai * bj
+            else:
+                out[k - n] -= ai * bj
+    return out
+
+
 # ---------------------------------------------------------------- helpers
 def crt(residues: Sequence[int], mods: Sequence[int]) -> int:
     M = math.prod(mods)

@@ -41,6 +41,7 @@ typedef struct {
 
 struct orc_ctx {
   uint32_t scheme, log_n, n, L, K, dnum, alpha, nB; /* nB = |Bsk| (BFV) */
+  uint32_t bfv_mult;                                /* ORC_BFV_BEHZ or ORC_BFV_HPS */
   uint64_t t;
   uint32_t nmod;
   orc_mod m[MAXM];
@@ -187,6 +188,12 @@ orc_ctx *orc_ctx_create(uint32_t scheme, uint32_t log_n, uint32_t L, uint32_t K,
   }
   for (uint32_t i = 0; i < c->nmod; ++i) mod_init(&c->m[i], qs[i], log_n);
   return c;
+}
+
+int orc_set_bfv_mult(orc_ctx *c, uint32_t method) {
+  if (method > ORC_BFV_HPS) return -1;
+  c->bfv_mult = method;
+  return 0;
 }
 
 void orc_ctx_destroy(orc_ctx *c) {
@@ -604,8 +611,127 @@ static void behz_floor_to_q(const orc_ctx *c, const behz_tab *B, const uint64_t 
   }
 }
 
-static void bfv_mul_relin_one(const orc_ctx *c, const behz_tab *B, const uint64_t *a, const uint64_t *b,
-                              const uint64_t *rlk, uint64_t *out) {
+/* ------------------------------------------------------------- BFV HPS */
+/* Halevi-Polyakov-Shoup (CT-RSA 2019, "An Improved RNS Variant of the BFV
+ * Homomorphic Encryption Scheme"), the multiplication technique OpenFHE's
+ * BFVrns offers as HPS, with the auxiliary base P = the Bsk primes:
+ *   1. exact extension of the centred lift Q -> P (section 2.4): y_i =
+ *      [x_i (Q/q_i)^-1]_{q_i}, v = floor(0.5 + sum_i y_i / q_i) in doubles,
+ *      x mod p_j = sum_i y_i [Q/q_i]_{p_j} - v [Q]_{p_j};
+ *   2. tensor in Q u P;
+ *   3. simple scaling by t/Q into P (section 4): with num_i = [t (Q/q_i)^-1]_{q_i},
+ *      round(t d / Q) mod p_j = sum_i x_i I_ij + floor(0.5 + sum_i x_i f_i)
+ *      + x_{p_j} [t Q^-1]_{p_j}, I_ij = [-num_i q_i^-1]_{p_j}, f_i = num_i / q_i;
+ *   4. P -> Q by the exact extension of step 1.
+ * Floating point: every double is one correctly rounded IEEE operation in a
+ * fixed order, no contraction (-ffp-contract=off), so the backend reproduces
+ * the same bits (oracle/bigint_model.py hps_* restates the same and checks the
+ * result against round(t d / Q) on integers). */
+typedef struct {
+  uint64_t qt[MAXM], qts[MAXM];        /* (Q/q_i)^-1 mod q_i + Shoup */
+  double invq[MAXM], frac[MAXM];       /* 1/q_i; num_i / q_i */
+  uint64_t qstar_p[MAXM][MAXM];        /* [Q/q_i]_{p_j} */
+  uint64_t Q_p[MAXM];                  /* [Q]_{p_j} */
+  uint64_t I[MAXM][MAXM];              /* [-num_i q_i^-1]_{p_j} */
+  uint64_t lam[MAXM];                  /* [t Q^-1]_{p_j} */
+  uint64_t pt[MAXM], pts[MAXM];        /* (P/p_j)^-1 mod p_j */
+  double invp[MAXM];
+  uint64_t pstar_q[MAXM][MAXM];        /* [P/p_j]_{q_i} */
+  uint64_t P_q[MAXM];                  /* [P]_{q_i} */
+} hps_tab;
+
+static void hps_init(const orc_ctx *c, hps_tab *H) {
+  const uint32_t L = c->L, nb = c->nB, bb = c->L + c->K;
+  for (uint32_t i = 0; i < L; ++i) {
+    const uint64_t q = c->m[i].q;
+    uint64_t h = 1;
+    for (uint32_t k = 0; k < L; ++k) if (k != i) h = mulmod(h, c->m[k].q % q, q);
+    H->qt[i] = invmod(h, q);
+    H->qts[i] = shoup_pre(H->qt[i], q);
+    H->invq[i] = 1.0 / (double)q;
+    const uint64_t num = mulmod(c->t % q, H->qt[i], q);
+    H->frac[i] = (double)num / (double)q;
+    for (uint32_t j = 0; j < nb; ++j) {
+      const uint64_t pj = c->m[bb + j].q;
+      uint64_t qs = 1;
+      for (uint32_t k = 0; k < L; ++k) if (k != i) qs = mulmod(qs, c->m[k].q % pj, pj);
+      H->qstar_p[i][j] = qs;
+      H->I[i][j] = mulmod((pj - num % pj) % pj, invmod(q % pj, pj), pj);
+    }
+  }
+  for (uint32_t j = 0; j < nb; ++j) {
+    const uint64_t pj = c->m[bb + j].q;
+    uint64_t Qm = 1, h = 1;
+    for (uint32_t k = 0; k < L; ++k) Qm = mulmod(Qm, c->m[k].q % pj, pj);
+    H->Q_p[j] = Qm;
+    H->lam[j] = mulmod(c->t % pj, invmod(Qm, pj), pj);
+    for (uint32_t k = 0; k < nb; ++k) if (k != j) h = mulmod(h, c->m[bb + k].q % pj, pj);
+    H->pt[j] = invmod(h, pj);
+    H->pts[j] = shoup_pre(H->pt[j], pj);
+    H->invp[j] = 1.0 / (double)pj;
+  }
+  for (uint32_t i = 0; i < L; ++i) {
+    const uint64_t q = c->m[i].q;
+    uint64_t Pm = 1;
+    for (uint32_t k = 0; k < nb; ++k) Pm = mulmod(Pm, c->m[bb + k].q % q, q);
+    H->P_q[i] = Pm;
+    for (uint32_t j = 0; j < nb; ++j) {
+      uint64_t ps = 1;
+      for (uint32_t k = 0; k < nb; ++k) if (k != j) ps = mulmod(ps, c->m[bb + k].q % q, q);
+      H->pstar_q[j][i] = ps;
+    }
+  }
+}
+
+/* x_q [L][N] coef -> x_p [nb][N] coef (the centred lift, exactly) */
+static void hps_extend(const orc_ctx *c, const hps_tab *H, const uint64_t *xq, uint64_t *xp) {
+  const uint32_t L = c->L, n = c->n, nb = c->nB, bb = c->L + c->K;
+  for (uint32_t k = 0; k < n; ++k) {
+    uint64_t y[MAXM];
+    double s = 0.0;
+    for (uint32_t i = 0; i < L; ++i) {
+      y[i] = shoup_mul(xq[(size_t)i * n + k], H->qt[i], H->qts[i], c->m[i].q);
+      s = s + (double)y[i] * H->invq[i];
+    }
+    const uint64_t v = (uint64_t)(s + 0.5);
+    for (uint32_t j = 0; j < nb; ++j) {
+      const uint64_t pj = c->m[bb + j].q;
+      u128 acc = 0;
+      for (uint32_t i = 0; i < L; ++i) acc += (u128)y[i] * H->qstar_p[i][j];
+      xp[(size_t)j * n + k] = submod((uint64_t)(acc % pj), mulmod(v % pj, H->Q_p[j], pj), pj);
+    }
+  }
+}
+
+/* d in Q u P (coef, canonical) -> round(t d / Q) in P -> Q */
+static void hps_scale_to_q(const orc_ctx *c, const hps_tab *H, const uint64_t *xq, const uint64_t *xp,
+                           uint64_t *out) {
+  const uint32_t L = c->L, n = c->n, nb = c->nB, bb = c->L + c->K;
+  for (uint32_t k = 0; k < n; ++k) {
+    double nu = 0.5;
+    for (uint32_t i = 0; i < L; ++i) nu = nu + (double)xq[(size_t)i * n + k] * H->frac[i];
+    const uint64_t r = (uint64_t)nu;
+    uint64_t y[MAXM];
+    double s = 0.0;
+    for (uint32_t j = 0; j < nb; ++j) {
+      const uint64_t pj = c->m[bb + j].q;
+      u128 acc = (u128)xp[(size_t)j * n + k] * H->lam[j] + r;
+      for (uint32_t i = 0; i < L; ++i) acc += (u128)xq[(size_t)i * n + k] * H->I[i][j];
+      y[j] = shoup_mul((uint64_t)(acc % pj), H->pt[j], H->pts[j], pj);
+      s = s + (double)y[j] * H->invp[j];
+    }
+    const uint64_t v = (uint64_t)(s + 0.5);
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint64_t q = c->m[i].q;
+      u128 acc = 0;
+      for (uint32_t j = 0; j < nb; ++j) acc += (u128)y[j] * H->pstar_q[j][i];
+      out[(size_t)i * n + k] = submod((uint64_t)(acc % q), mulmod(v % q, H->P_q[i], q), q);
+    }
+  }
+}
+
+static void bfv_mul_relin_one(const orc_ctx *c, const behz_tab *B, const hps_tab *H, const uint64_t *a,
+                              const uint64_t *b, const uint64_t *rlk, uint64_t *out) {
   const uint32_t L = c->L, n = c->n, nb = c->nB, bb = c->L + c->K;
   const size_t LN = (size_t)L * n, BN = (size_t)nb * n;
   uint64_t *xq = malloc(sizeof(uint64_t) * 4 * LN), *xb = malloc(sizeof(uint64_t) * 4 * BN);
@@ -613,7 +739,8 @@ static void bfv_mul_relin_one(const orc_ctx *c, const behz_tab *B, const uint64_
   const uint64_t *in[4] = {a, a + LN, b, b + LN};
   for (int p = 0; p < 4; ++p) {
     memcpy(xq + p * LN, in[p], sizeof(uint64_t) * LN);
-    behz_extend(c, B, in[p], xb + p * BN);
+    if (H) hps_extend(c, H, in[p], xb + p * BN);
+    else behz_extend(c, B, in[p], xb + p * BN);
   }
   orc_ntt_fwd(c, xq, 4, 0, L);
   orc_ntt_fwd(c, xb, 4, bb, nb);
@@ -639,7 +766,10 @@ static void bfv_mul_relin_one(const orc_ctx *c, const behz_tab *B, const uint64_
   orc_ntt_inv(c, eb, 3, bb, nb);
   /* 3. scale by t/Q with flooring, back to Q */
   uint64_t *r = malloc(sizeof(uint64_t) * 3 * LN);
-  for (int p = 0; p < 3; ++p) behz_floor_to_q(c, B, eq + p * LN, eb + p * BN, r + p * LN);
+  for (int p = 0; p < 3; ++p) {
+    if (H) hps_scale_to_q(c, H, eq + p * LN, eb + p * BN, r + p * LN);
+    else behz_floor_to_q(c, B, eq + p * LN, eb + p * BN, r + p * LN);
+  }
   /* 4. relinearize r2 */
   uint64_t *ks = malloc(sizeof(uint64_t) * 2 * LN);
   keyswitch_one(c, r + 2 * LN, rlk, ks, 0);
@@ -673,16 +803,23 @@ void orc_mul_relin(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const
                    uint64_t *out, uint32_t n_ct) {
   const size_t L = c->L, N = c->n, CT = 2 * L * N;
   behz_tab *B = NULL;
+  hps_tab *H = NULL;
   if (c->scheme == ORC_SCHEME_BFV) {
-    B = malloc(sizeof(behz_tab));
-    behz_init(c, B);
+    if (c->bfv_mult == ORC_BFV_HPS) {
+      H = malloc(sizeof(hps_tab));
+      hps_init(c, H);
+    } else {
+      B = malloc(sizeof(behz_tab));
+      behz_init(c, B);
+    }
   }
 #pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
   for (long i = 0; i < (long)n_ct; ++i) {
-    if (B) bfv_mul_relin_one(c, B, a + i * CT, b + i * CT, rlk, out + i * CT);
+    if (c->scheme == ORC_SCHEME_BFV) bfv_mul_relin_one(c, B, H, a + i * CT, b + i * CT, rlk, out + i * CT);
     else ckks_mul_relin_one(c, a + i * CT, b + i * CT, rlk, out + i * CT, c->L);
   }
   free(B);
+  free(H);
 }
 
 static void rotate_lvl(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,

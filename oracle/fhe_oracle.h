@@ -56,6 +56,11 @@ uint64_t orc_psi(const orc_ctx *c, uint32_t mod_idx);
 uint32_t orc_gen_primes(uint32_t bits, uint32_t log_n, uint32_t count,
                         const uint64_t *excl, uint32_t n_excl, uint64_t *out);
 void orc_set_threads(int n);
+/* BFV multiplication technique: BEHZ (SEAL RNSTool form, the default) or HPS
+ * (Halevi-Polyakov-Shoup, OpenFHE BFVrns "HPS"); returns 0, or -1 if unknown */
+#define ORC_BFV_BEHZ 0u
+#define ORC_BFV_HPS 1u
+int orc_set_bfv_mult(orc_ctx *c, uint32_t method);
 
 /* ---- primitive RNS ops: data [n_polys][n_limbs][N], limb l uses modulus mod_begin+l */
 void orc_ntt_fwd(const orc_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin, uint32_t n_limbs);

@@ -102,6 +102,24 @@ def gen_bfv(rng):
              out_mul=arr(out_mul), out_add=arr(out_add), g=np.uint32(g), out_rot=arr(out_rot))
 
 
+def gen_bfv_hps(rng):
+    """BFV mul+relin by HPS (oracle/bigint_model.py bfv_mul_relin_hps, which also
+    checks each scaled tensor output against round(t d / Q) on integers)."""
+    log_n, L, K, dnum, t = 10, 4, 2, 2, 65537
+    n = 1 << log_n
+    Q = M.gen_primes(60, log_n, L)
+    P = M.gen_primes(61, log_n, K, exclude=Q)
+    Bsk = M.gen_primes(61, log_n, L + 1, exclude=Q + P)
+    p = M.Params(log_n, L, K, dnum, Q + P + Bsk, "bfv", t)
+    a = [rand_limbs(rng, Q, n) for _ in range(2)]
+    b = [rand_limbs(rng, Q, n) for _ in range(2)]
+    rlk = [[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(dnum)]
+    out_mul = M.bfv_mul_relin_hps(p, a, b, rlk)
+    np.savez(os.path.join(HERE, "bfv_hps_n1024_l4.npz"), log_n=np.uint32(log_n), L=np.uint32(L), K=np.uint32(K),
+             dnum=np.uint32(dnum), t=np.uint64(t), moduli=arr(Q + P + Bsk), a=arr(a), b=arr(b), rlk=arr(rlk),
+             out_mul=arr(out_mul))
+
+
 def gen_ckks_levels(rng):
     """CKKS at reduced levels: L = 5 primes, alpha = 3 (dnum 2), so level 4 has
     a partial second digit, level 3 one full digit and level 2 one partial
@@ -140,11 +158,14 @@ def main():
     gen_ckks(rng)
     gen_bfv(rng)
     gen_ckks_levels(random.Random(0x4C564C53))
+    gen_bfv_hps(random.Random(0x485053))
     print("golden vectors written to", HERE)
 
 
 if __name__ == "__main__":
     if sys.argv[1:] == ["levels"]:  # only the level fixture (the others are unchanged)
         gen_ckks_levels(random.Random(0x4C564C53))
+    elif sys.argv[1:] == ["hps"]:
+        gen_bfv_hps(random.Random(0x485053))
     else:
         main()

@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(ORACLE_DIR, "build", "libfhe_oracle.so")
 
 SCHEME_CKKS = 0
 SCHEME_BFV = 1
+BFV_MULT = {"behz": 0, "hps": 1}
 
 _u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
 _i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
@@ -45,6 +46,7 @@ def lib():
         "orc_psi": (u64, [vp, u32]),
         "orc_gen_primes": (u32, [u32, u32, u32, C.c_void_p, u32, _u64p]),
         "orc_set_threads": (None, [C.c_int]),
+        "orc_set_bfv_mult": (C.c_int, [vp, u32]),
         "orc_ntt_fwd": (None, [vp, _u64p, u32, u32, u32]),
         "orc_ntt_inv": (None, [vp, _u64p, u32, u32, u32]),
         "orc_add": (None, [vp, _u64p, _u64p, _u64p, u32, u32, u32]),
@@ -81,7 +83,7 @@ class Oracle:
     """Thin object wrapper mirroring the backend's context."""
 
     def __init__(self, scheme: int, log_n: int, L: int, K: int = 0, dnum: int = 1,
-                 q_bits: int = 60, p_bits: int = 61, t: int = 0, moduli=None):
+                 q_bits: int = 60, p_bits: int = 61, t: int = 0, moduli=None, bfv_mult: str = "behz"):
         self.lib = lib()
         self.scheme, self.log_n, self.n = scheme, log_n, 1 << log_n
         self.L, self.K, self.dnum, self.t = L, K, dnum, t
@@ -93,6 +95,8 @@ class Oracle:
         self.h = self.lib.orc_ctx_create(scheme, log_n, L, K, dnum, q_bits, p_bits, t, mp)
         if not self.h:
             raise ValueError("orc_ctx_create failed")
+        if bfv_mult not in ("behz", "hps") or self.lib.orc_set_bfv_mult(self.h, BFV_MULT[bfv_mult]) != 0:
+            raise ValueError(f"unknown BFV multiplication technique {bfv_mult!r}")
         nm = self.lib.orc_num_moduli(self.h)
         self.moduli = np.zeros(nm, dtype=np.uint64)
         self.lib.orc_moduli(self.h, self.moduli)

@@ -119,3 +119,13 @@ def test_full_level_calls_match_level_calls():
     L = int(g["L"])
     assert np.array_equal(o.mul_relin_at(g["a"][None], g["b"][None], g["rlk"], L),
                           o.mul_relin(g["a"][None], g["b"][None], g["rlk"]))
+
+
+def test_bfv_hps_mul_relin_golden():
+    """HPS multiplication (float parts bit-identical to the big-int model's
+    restatement, which checks round(t d / Q) on integers)."""
+    g = load("bfv_hps_n1024_l4.npz")
+    o = Oracle(SCHEME_BFV, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), t=int(g["t"]),
+               moduli=g["moduli"], bfv_mult="hps")
+    out = o.mul_relin(g["a"][None], g["b"][None], g["rlk"])
+    assert np.array_equal(out[0], g["out_mul"])

@@ -9,6 +9,7 @@ import math
 import random
 
 import numpy as np
+import pytest
 
 from fhe_math import automorph_int, crt_centered, negacyclic_int, to_rns
 from oracle_ffi import Oracle, SCHEME_BFV, SCHEME_CKKS
@@ -65,9 +66,10 @@ def test_ckks_rotate_decrypts():
         assert err < 2 ** 30, (steps, math.log2(err + 1))
 
 
-def test_bfv_mul_relin_decrypts_exactly():
+@pytest.mark.parametrize("mult", ["behz", "hps"])
+def test_bfv_mul_relin_decrypts_exactly(mult):
     t = 65537
-    o = Oracle(SCHEME_BFV, 10, 4, 2, 2, t=t)
+    o = Oracle(SCHEME_BFV, 10, 4, 2, 2, t=t, bfv_mult=mult)
     Q = [int(q) for q in o.moduli[:o.L]]
     Qp = math.prod(Q)
     s, s_qp = _keys(o)
