@@ -299,6 +299,7 @@ def main():
         "launch_ms": round(ntt_ms, 4),
     }
     roof.update(profile_fields(args.profile_json, limbs, algo_per_limb))
+    roof.update(copy_cap_fields(roof["frac"]))
 
     secondary = None
     if full_secondary:
@@ -343,6 +344,7 @@ def main():
             "per_rank_check": {"case": SELF_CHECK["case"], "lanes": [v["lanes"] for v in per_rank_ok],
                                "source": "tests/golden/digests.json (CPU oracle, make_digests.py)"},
             "algorithmic_GBps_ct_mult": round(value / n_gpus * 6 * L * n * 8 / 1e9, 1),
+            "step": step_fields(value / n_gpus, 6 * L * n * 8),
             "cpu_baseline": cpu,
             "secondary": secondary,
         }
@@ -491,6 +493,44 @@ def profile_fields(path, limbs, algo_per_limb):
         res["frac_rocprof"] = round(plimbs * algo_per_limb / (launch_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
     if pj.get("valu_busy") is not None:
         res["valu_busy"] = pj["valu_busy"]
+    return res
+
+
+def copy_cap_fields(frac):
+    """What the roofline kernel can reach with its access pattern: a two-pass NTT
+    moves every word through HBM twice, and a pure copy with the column-pass and
+    row-pass patterns (profiles/copy_cap.json, committed microbenchmark) bounds
+    each pass.  cap_frac = algorithmic bytes / (both copy times) / peak."""
+    try:
+        cc = json.load(open(os.path.join(ROOT, "profiles", "copy_cap.json")))
+    except (OSError, ValueError):
+        return {}
+    algo = cc["limbs"] * 2 * (1 << LOG_N) * 8
+    cap = algo / ((cc["col_pass_copy_ms"] + cc["row_pass_copy_ms"]) * 1e-3) / 1e9 / HBM_PEAK_GBS
+    return {"cap_frac": round(cap, 4), "frac_of_cap": round(frac / cap, 4),
+            "bound_note": "HBM with the two-pass access pattern (column pass of 128 B row segments, then row "
+                          "pass): cap_frac is a pure copy with those patterns; VALU co-bound (valu_busy)",
+            "cap_source": "profiles/copy_cap.json (" + cc["source"] + ")"}
+
+
+def step_fields(per_gpu_value, algo_bytes_per_ct):
+    """The headline op's own roofline: HBM bytes per ct-mult
+    counted by rocprofv3 (FETCH_SIZE x2 + WRITE_SIZE over every kernel of a
+    128-ct mul+relin wave, profiles/step_traffic.json, tools/step_summary.py),
+    the fraction of peak the measured headline rate moves with those bytes and
+    with the algorithmic ones, and the dominant kernel of the wave."""
+    res = {"algorithmic_bytes_per_ct_mult": algo_bytes_per_ct,
+           "headline_frac_algorithmic": round(per_gpu_value * algo_bytes_per_ct / 1e9 / HBM_PEAK_GBS, 4)}
+    try:
+        st = json.load(open(os.path.join(ROOT, "profiles", "step_traffic.json")))
+    except (OSError, ValueError):
+        return res
+    b = st["hbm_bytes_per_ct_mult"]
+    res.update({"hbm_bytes_per_ct_mult": b,
+                "headline_GBps_counted_bytes": round(per_gpu_value * b / 1e9, 1),
+                "headline_frac_counted_bytes": round(per_gpu_value * b / 1e9 / HBM_PEAK_GBS, 4),
+                "wave_kernel_ms": st["kernel_ms_per_wave"], "wave_kernel_TBps": st["kernel_TBps"],
+                "dominant_kernel": st["dominant"], "source": st["source"] + " (rocprofv3, committed)"})
     return res
 
 

@@ -19,6 +19,7 @@ SCHEME_BFV = 1
 
 FHE_OK = 0
 FHE_ERR_INVALID, FHE_ERR_DEVICE, FHE_ERR_OOM, FHE_ERR_UNSUPPORTED = -1, -2, -3, -4
+FHE_FLAG_BFV_HPS = 1
 _ERRORS = {FHE_ERR_INVALID: "FHE_ERR_INVALID", FHE_ERR_DEVICE: "FHE_ERR_DEVICE", FHE_ERR_OOM: "FHE_ERR_OOM",
            FHE_ERR_UNSUPPORTED: "FHE_ERR_UNSUPPORTED"}
 
@@ -36,7 +37,7 @@ class _Params(C.Structure):
         ("dnum", C.c_uint32),
         ("q_bits", C.c_uint32),
         ("p_bits", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("flags", C.c_uint32),
         ("plain_modulus", C.c_uint64),
         ("moduli", C.c_void_p),
     ]
@@ -135,7 +136,8 @@ class Context:
     """One device context (params + twiddle/CRT tables + workspace)."""
 
     def __init__(self, scheme: int, log_n: int, L: int, K: int = 0, dnum: int = 1, q_bits: int = 60,
-                 p_bits: int = 61, t: int = 0, moduli: Optional[Sequence[int]] = None, device: int = 0):
+                 p_bits: int = 61, t: int = 0, moduli: Optional[Sequence[int]] = None, device: int = 0,
+                 bfv_mult: str = "behz"):
         self.lib = load_library()
         self.scheme, self.log_n, self.n = scheme, log_n, 1 << log_n
         self.L, self.K, self.dnum, self.t = L, K, dnum, t
@@ -145,7 +147,11 @@ class Context:
         if moduli is not None:
             self._mods_keep = np.ascontiguousarray(np.asarray(moduli, dtype=np.uint64))
             mp = self._mods_keep.ctypes.data
-        p = _Params(scheme, log_n, L, K, dnum, q_bits, p_bits, 0, t, mp)
+        if bfv_mult not in ("behz", "hps"):
+            raise FheBackendError(f"unknown BFV multiplication technique {bfv_mult!r} (behz or hps)")
+        self.bfv_mult = bfv_mult
+        flags = FHE_FLAG_BFV_HPS if bfv_mult == "hps" else 0
+        p = _Params(scheme, log_n, L, K, dnum, q_bits, p_bits, flags, t, mp)
         h = C.c_void_p()
         rc = self.lib.fhe_ctx_create(C.byref(p), device, C.byref(h))
         if rc != FHE_OK:

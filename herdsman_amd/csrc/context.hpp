@@ -84,6 +84,7 @@ struct fhe_ctx {
   std::vector<ConvTab> modup_tabs;  // host copies of d_modup (device pointers inside)
   std::vector<void *> blobs;   // device allocations owned by the context
   void *behz = nullptr;        // BEHZ device constants (BFV)
+  void *hps = nullptr;         // HPS device constants (BFV with FHE_FLAG_BFV_HPS): BFV mul uses HPS
   // fhe_base_conv tables by (src ids, ~0, dst ids); their device arrays are
   // blobs of this context, so they are freed with it
   std::map<std::vector<u32>, ConvTab> conv_cache;
@@ -202,5 +203,6 @@ int rescale_impl(fhe_ctx *up, fhe_ctx *lo, const u64 *ct, u64 *out, u32 n);
 size_t rescale_ws_bytes(const fhe_ctx *lo, u32 n);
 int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n_ct);
 int behz_setup(fhe_ctx *c);
+int hps_setup(fhe_ctx *c);
 size_t keyswitch_ws_bytes(const fhe_ctx *c, u32 n);
 size_t bfv_mul_ws_bytes(const fhe_ctx *c, u32 n);

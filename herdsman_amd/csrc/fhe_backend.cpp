@@ -312,7 +312,7 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p, u32 alpha = 0) {
     }
   }
   if (p->scheme == FHE_SCHEME_BFV) {
-    int rc = behz_setup(c);
+    int rc = (p->flags & FHE_FLAG_BFV_HPS) ? hps_setup(c) : behz_setup(c);
     if (rc) return rc;
   }
   return FHE_OK;

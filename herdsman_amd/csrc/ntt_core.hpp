@@ -64,15 +64,6 @@
 #ifndef AUT_PD
 #define AUT_PD 2  // PRO_AUTOMORPH gather prefetch depth (elements)
 #endif
-#ifndef CONV_T
-#define CONV_T 1  // PRO_CONV target limbs per workgroup (conv_multi_body); 2 as first written spilled 34-98 VGPRs: headline 15.8k against 18.2k
-#endif
-#ifndef CONV_PIPE
-#define CONV_PIPE 2  // conv_multi_body: source-load prefetch depth (elements)
-#endif
-#ifndef CONV_BUF
-#define CONV_BUF 0  // PRO_CONV (one target per workgroup): >0 buffer loads of the sources, that many elements ahead
-#endif
 #ifndef MODUP_COL_SPLIT
 #define MODUP_COL_SPLIT 1
 #endif
@@ -732,34 +723,6 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       u32 hc0[NS], hc1[NS];  // the constants' 31-bit digits (uniform, SGPRs)
 #pragma unroll
       for (int i = 0; i < NS; ++i) split31(ep.h[i], hc0[i], hc1[i]);
-#if CONV_BUF
-      // buffer loads over the NS source limbs (one descriptor, 32-bit voffset,
-      // scalar soffset per (source, element)), CONV_BUF elements in flight; the
-      // loads of element r + PD carry a false dependence on element r - 1's
-      // result so the compiler cannot hoist them all (see conv_multi_body)
-      constexpr int PD = CONV_BUF;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void *)ep.src, 0, (u32)(NS * NW * 8), 0x00020000);
-      u32 voff_dep = voff;
-      u64 sv[PD + 1][NS];
-      const auto load_el = [&](u64(&d)[NS], int r) {
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b64(
-              rs, voff_dep, (u32)(i * NW * 8) + ((u32)GF::k_reg(r) << (PG::LS + 3)), 0);
-          d[i] = ((u64)v[1] << 32) | v[0];
-        }
-      };
-#pragma unroll
-      for (int r = 0; r < PD; ++r) load_el(sv[r], r);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (r + PD < R) load_el(sv[(r + PD) % (PD + 1)], r + PD);
-        x[r] = CONV_COLS && SP && WIDE && CONV_SP60 ? dot_cols_sp60<NS>(sv[r % (PD + 1)], hc0, hc1, mi.q_hi)
-                                                    : dot_cols<NS, SP>(sv[r % (PD + 1)], hc0, hc1, mi);
-        asm volatile("" : "+v"(voff_dep) : "v"(x[r]));
-      }
-#else
 #pragma unroll
       for (int c0 = 0; c0 < R; c0 += 4) {
         u64 sv[4][NS];
@@ -774,7 +737,6 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
                       : CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                                  // < 2q
                                   : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);                   // < 4q
       }
-#endif
     } else {
       // the first forward pass may read out of place (NttArgs::src)
       const u64 *din = data;
@@ -795,112 +757,8 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
   group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, 0>(x, tc, lds, tw, data, voff, w, ts, hi, a, mi, mod, ep);
 }
 
-// PRO_CONV with CT target limbs per workgroup (round 4): the NS source words of
-// an element are loaded (and split into 31-bit digits) once and feed the CT
-// targets' dot products; target 0's transform runs while the other targets'
-// 16-word input tiles wait in VGPRs, then each following target's transform
-// starts from registers (no load phase).  One target per workgroup made every
-// target re-load all NS sources: NS L2 reads per element per target.
-template <int LOG_N, int S, int LOGR, int W, bool SP, bool WIDE, int EPI, int CT>
-__device__ __forceinline__ void conv_multi_body(const NttArgs &a, u64 *lds, u32 poly, u32 grp, u32 w, u32 ts,
-                                                u32 hi, u32 gb) {
-  using PG = PassGeo<LOG_N, S, true, false>;
-  constexpr int R = 1 << LOGR;
-  constexpr int NG = (S + LOGR - 1) / LOGR;
-  constexpr int NS = conv_ns(EPI);
-  constexpr size_t NW = (size_t)1 << LOG_N;
-  using GF = Grp<S, LOGR, 0>;
-  const u32 t0 = grp * CT;
-  const u32 nt = min((u32)CT, a.map.cnt - t0);  // uniform
-  u32 hc0[CT][NS], hc1[CT][NS];
-  u32 q_hi[CT];
-  ModInfo mt[CT];
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const u32 act = t0 + ((u32)t < nt ? t : 0);
-    mt[t] = a.mods[a.map.mod_offset + limbmap_limb(a.map, act)];
-    q_hi[t] = mt[t].q_hi;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) split31(a.c_h[(size_t)i * a.c_nd + act], hc0[t][i], hc1[t][i]);
-  }
-  // group 0 of a forward column pass (stages 0-3, hi = 0, ts >> p = 0) uses the
-  // 15 twiddles tw[1..15] of its modulus in every thread: read them here, before
-  // any store, so they are scalar loads held in SGPRs for every target
-  static_assert(PG::S0 == 0 && Grp<S, LOGR, 0>::p == S - LOGR && (W << (S - LOGR)) <= (W << Grp<S, LOGR, 0>::p),
-                "group 0 twiddles are uniform");
-  u64 tz[CT][16];
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const u32 act = t0 + ((u32)t < nt ? t : 0);
-    const u64 *twt = a.tw + ((size_t)(a.map.mod_offset + limbmap_limb(a.map, act)) << LOG_N);
-#pragma unroll
-    for (int k = 0; k < 15; ++k) tz[t][k] = twt[k + 1];
-    tz[t][15] = 0;
-  }
-  const u64 *src = a.c_src + (((size_t)poly * a.c_src_stride + a.c_src_first) << LOG_N);
-  const u32 voff_in = (gb + (GF::k_thr(ts) << PG::LS)) << 3;
-  u64 x[CT][R];
-  // the NS source words of element r + PD are in flight while element r's CT
-  // dot products run (PD + 1 element buffers of NS words): the whole 16-element
-  // prologue hoisted would need 2 NS R VGPRs on top of the CT R outputs
-  constexpr int PD = CONV_PIPE;
-  u64 sv[PD + 1][NS];
-  // element r of source i through ONE buffer descriptor over the NS source
-  // limbs: the per-thread part is the single 32-bit voffset, the (source,
-  // element) part a scalar soffset.  With global loads the compiler folds those
-  // offsets into 64-bit VGPR addresses (two VALU adds and two VGPRs per load)
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, (u32)(NS * NW * 8), 0x00020000);
-  // The loads of element r + PD carry a false dependence on element r - 1's
-  // result (voff_dep): the source words are invariant loads, which the
-  // compiler otherwise hoists all at once (64 in flight for NS = 4, and the
-  // outputs spill)
-  u32 voff_dep = voff_in;
-  const auto load_el = [&](u64(&d)[NS], int r) {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(
-          rs, voff_dep, (u32)(i * NW * 8) + ((u32)GF::k_reg(r) << (PG::LS + 3)), 0);
-      d[i] = ((u64)v[1] << 32) | v[0];
-    }
-  };
-#pragma unroll
-  for (int r = 0; r < PD; ++r) load_el(sv[r], r);
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if (r + PD < R) load_el(sv[(r + PD) % (PD + 1)], r + PD);
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-      x[t][r] = CONV_COLS && SP && WIDE && CONV_SP60 ? dot_cols_sp60<NS>(sv[r % (PD + 1)], hc0[t], hc1[t], q_hi[t])
-                                                     : dot_cols<NS, SP>(sv[r % (PD + 1)], hc0[t], hc1[t], mt[t]);  // < 2q
-    asm volatile("" : "+v"(voff_dep) : "v"(x[CT - 1][r]));
-  }
-  const u32 voff = (gb + (Grp<S, LOGR, NG - 1>::k_thr(ts) << PG::LS)) << 3;
-  const EpiRow ep{};
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    if ((u32)t >= nt) break;
-    if (t) __syncthreads();  // the previous target's last exchange has been read
-    const u32 limb = limbmap_limb(a.map, t0 + t);
-    const u32 mod = a.map.mod_offset + limb;
-    u64 *data = a.map.base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
-    const u64 *tw = a.tw + ((size_t)mod << LOG_N);
-    u64(&tc)[16] = tz[t];
-#ifdef CONV_DIAG
-    for (int r = 0; r < R; ++r) st_b(data + ((size_t)r << PG::LS), voff, x[t][r] + tc[r]);
-#else
-    group_loop<LOG_N, S, LOGR, W, false, true, SP, WIDE, EPI_NONE, 0>(x[t], tc, lds, tw, data, voff, w, ts, hi, a,
-                                                                     mt[t], mod, ep);
-#endif
-  }
-}
-
-
 #ifndef NTT_MINW
 #define NTT_MINW 1
-#endif
-#ifndef CONV_MINW
-#define CONV_MINW 4  // conv_multi_body: the LDS tile allows 4 waves per SIMD; without a bound the
-                     // compiler hoists every source load (130-226 VGPRs, 2-3 waves)
 #endif
 // WM (forward passes): the lazy schedule of the launch's moduli, chosen on the
 // host (wide_mode): 1 all WIDE (q < 2^60), 0 all narrow, 2 mixed (a per-
@@ -909,7 +767,7 @@ __device__ __forceinline__ void conv_multi_body(const NttArgs &a, u64 *lds, u32 
 // LDS allows: a launch over one modulus class avoids it)
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int WM>
 __global__ void __launch_bounds__(W << (S - LOGR),
-                                  (W << (S - LOGR)) == 256 ? (is_conv(EPI) && CONV_T > 1 ? CONV_MINW : NTT_MINW) : 1)
+                                  (W << (S - LOGR)) == 256 ? NTT_MINW : 1)
     ntt_pass(NttArgs a) {
   static_assert(is_combine(EPI) || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
                     EPI == PRO_BFVT || is_conv(EPI) || is_ksp(EPI),
@@ -982,18 +840,6 @@ __global__ void __launch_bounds__(W << (S - LOGR),
     }
     bx = sb % cbs;
     poly = sb / cbs;
-    if constexpr (CONV_T > 1) {
-      // act = target group (CONV_T target limbs)
-      u32 w = tid % W, ts = tid / W;
-      constexpr u32 stride = 1u << PG::LS;
-      const u32 u = bx * W + w;
-      const u32 hi = u >> PG::LS;
-      const u32 gb = (hi << (S + PG::LS)) + (u & (stride - 1));
-      // mixed moduli classes (WM 2) take the narrow schedule, valid for every target
-      constexpr bool WIDE_C = !INV && WM == 1;
-      conv_multi_body<LOG_N, S, LOGR, W, SP, WIDE_C, EPI, CONV_T>(a, lds, poly, act, w, ts, hi, gb);
-      return;
-    }
   }
   const u32 limb = limbmap_limb(a.map, act);
   const u32 mod = a.map.mod_offset + limb;
@@ -1098,8 +944,7 @@ int launch_one(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
   constexpr u32 subs = 1u << (LOG_N - S);
   // dispatch order: row blocks, then polys, then limbs -- the resident
   // workgroups share one modulus, so its twiddle table stays in L2
-  // (conversion prologue: gridDim.z counts groups of CONV_T target limbs)
-  dim3 grid(subs / W, n_jobs / a.map.cnt, is_conv(EPI) ? (a.map.cnt + CONV_T - 1) / CONV_T : a.map.cnt);
+  dim3 grid(subs / W, n_jobs / a.map.cnt, a.map.cnt);
   auto k = ntt_pass<LOG_N, S, LOGR, W, INV, COLS, SP, EPI, WM>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, c->stream, a);

@@ -455,6 +455,135 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   }
 }
 
+// ------------------------------------------------------------------ HPS
+// BFV multiplication by Halevi-Polyakov-Shoup (oracle hps_*; OpenFHE BFVrns
+// "HPS"), auxiliary base P = the Bsk primes.  Same pipeline as BEHZ (the two
+// kernels below replace behz_extend / behz_floor; NTT, tensor and relinearise
+// are shared).  The doubles are single rounded IEEE operations in the oracle's
+// order: fp contraction is off in these kernels (no v_fma_f64), u64 -> f64 is
+// round-to-nearest as in C, and the truncations are floor of positive values.
+struct HpsDev {
+  u32 L, nB, bsk0;
+  u64 qt_R[BEHZ_MAXL];                   // (Q/q_i)^-1 R mod q_i
+  double invq[BEHZ_MAXL];                // 1 / q_i
+  u64 qstar_R[BEHZ_MAXL][BEHZ_MAXL + 1];  // [Q/q_i]_{p_j} R
+  u64 Q_R[BEHZ_MAXL + 1];                // Q R mod p_j
+  u64 ninv_R[BEHZ_MAXL];                 // N^-1 R mod q_i (the tensor's INTT skips N^-1)
+  double frac[BEHZ_MAXL];                // num_i / q_i, num_i = [t (Q/q_i)^-1]_{q_i}
+  u64 I_R[BEHZ_MAXL][BEHZ_MAXL + 1];     // [-num_i q_i^-1]_{p_j} R
+  u64 lam_R[BEHZ_MAXL + 1];              // t Q^-1 N^-1 R mod p_j (applied to the unscaled e_{p_j})
+  u64 pt_R[BEHZ_MAXL + 1];               // (P/p_j)^-1 R mod p_j
+  double invp[BEHZ_MAXL + 1];            // 1 / p_j
+  u64 pstar_R[BEHZ_MAXL + 1][BEHZ_MAXL];  // [P/p_j]_{q_i} R
+  u64 P_R[BEHZ_MAXL];                    // P R mod q_i
+};
+
+// floor(s + 0.5) and floor(s) of a non-negative double, as the oracle's (u64) casts
+__device__ __forceinline__ u64 hps_round(double s) {
+#pragma clang fp contract(off)
+  return (u64)(s + 0.5);
+}
+__device__ __forceinline__ u64 hps_round_down(double s) { return (u64)s; }
+
+// init + sum_i y_i * w_i, left to right, each product and each sum rounded
+template <int NL, bool EX>
+__device__ __forceinline__ double hps_fsum(const u64 (&y)[NL], const double *w, u32 n, double init) {
+#pragma clang fp contract(off)
+  double s = init;
+#pragma unroll
+  for (int i = 0; i < NL; ++i)
+    if (EX || i < (int)n) s = s + (double)y[i] * w[i];
+  return s;
+}
+
+// Q -> P, the exact extension of the centred lift: y_i = [x_i (Q/q_i)^-1],
+// v = floor(0.5 + sum y_i / q_i), x mod p_j = sum_i y_i [Q/q_i]_{p_j} - v [Q]_{p_j}.
+// Layout as behz_extend_kernel (xb [2][n][2][nB][N]).
+template <int NL, bool SP, bool EX>
+__global__ void __launch_bounds__(EW_BLOCK) hps_extend_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
+                                                              u64 *__restrict__ xb, const HpsDev *hp,
+                                                              const ModInfo *mods, u32 log_n, u32 n_items) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 p = blockIdx.y, item = p >> 2, w = p & 3;
+  const size_t N = (size_t)1 << log_n;
+  const u32 L = EX ? NL : hp->L, nB = L + 1;
+  const u64 *s = (w < 2 ? a : b) + ((size_t)(2 * item + (w & 1)) * L) * N + k;
+  u64 y[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    y[i] = 0;
+    if (EX || i < (int)L) {
+      const ModInfo m = mods[i];
+      y[i] = csub63(mont_mul<SP>(ld_nt(s + i * N), hp->qt_R[i], m), m.q);
+    }
+  }
+  const u64 v = hps_round(hps_fsum<NL, EX>(y, hp->invq, L, 0.0));
+  u64 *d = xb + ((size_t)((w >> 1) * n_items + item) * 2 + (w & 1)) * nB * N + k;
+  constexpr int UJ = EX ? NL + 1 : 1;
+#pragma unroll UJ
+  for (int j = 0; j < NL + 1; ++j) {
+    if (EX || j < (int)nB) {
+      const ModInfo m = mods[hp->bsk0 + j];
+      const u64 x = dot_mont<NL, SP>(y, &hp->qstar_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 vq = csub63(mont_mul<SP>(v, hp->Q_R[j], m), m.q);
+      d[j * N] = sub_mod(x, vq, m.q);
+    }
+  }
+}
+
+// d in Q u P (coefficient form, INTT without N^-1) -> round(t d / Q) in P ->
+// Q.  In P: z_j = sum_i x_i I_ij + e_{p_j} t Q^-1 N^-1 + [r]_{p_j}, r =
+// floor(0.5 + sum x_i f_i) (x_i = d mod q_i, the INTT's N^-1 applied first);
+// then y_j = [z_j (P/p_j)^-1], v = floor(0.5 + sum y_j / p_j) and
+// out_i = sum_j y_j [P/p_j]_{q_i} - v [P]_{q_i}.  Outputs as behz_floor_kernel
+// (r0, r1 -> out01; r2 -> dc and its own-digit ext slot times R).
+template <int NL, bool SP, bool EX>
+__global__ void __launch_bounds__(EW_BLOCK) hps_scale_kernel(const u64 *__restrict__ eq, const u64 *__restrict__ eb,
+                                                             u64 *__restrict__ out01, u64 *__restrict__ dc,
+                                                             u64 *__restrict__ ext, const HpsDev *hp,
+                                                             const ModInfo *mods, u32 log_n, u32 QP, u32 dig_len,
+                                                             u32 ndig) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 ct = blockIdx.y / 3, p = blockIdx.y % 3;
+  const size_t N = (size_t)1 << log_n;
+  const u32 L = EX ? NL : hp->L, nB = L + 1;
+  const u64 *xq = eq + ((size_t)(ct * 3 + p) * L) * N + k;
+  const u64 *xb = eb + ((size_t)(ct * 3 + p) * nB) * N + k;
+  u64 x[NL];  // d mod q_i, canonical
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    x[i] = 0;
+    if (EX || i < (int)L) {
+      const ModInfo m = mods[i];
+      x[i] = csub63(mont_mul<SP>(ld_nt(xq + i * N), hp->ninv_R[i], m), m.q);
+    }
+  }
+  const u64 r = hps_round_down(hps_fsum<NL, EX>(x, hp->frac, L, 0.5));  // < L 2^61
+  u64 y[NL + 1];
+  constexpr int UJ = EX ? NL + 1 : 1;
+#pragma unroll UJ
+  for (int j = 0; j < NL + 1; ++j) {
+    y[j] = 0;
+    if (EX || j < (int)nB) {
+      const ModInfo m = mods[hp->bsk0 + j];
+      const u64 zi = dot_mont<NL, SP>(x, &hp->I_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 zp = csub63(mont_mul<SP>(ld_nt(xb + j * N), hp->lam_R[j], m), m.q);
+      const u64 zj = add_mod(add_mod(zi, zp, m.q), reduce128<SP>(U128{r, 0}, m), m.q);
+      y[j] = csub63(mont_mul<SP>(zj, hp->pt_R[j], m), m.q);
+    }
+  }
+  const u64 v = hps_round(hps_fsum<NL + 1, EX>(y, hp->invp, nB, 0.0));
+  u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
+  for (int i = 0; i < (EX ? NL : (int)L); ++i) {
+    const ModInfo m = mods[i];
+    const u64 cq = dot_mont<NL + 1, SP>(y, &hp->pstar_R[0][i], BEHZ_MAXL, nB, m);
+    const u64 vp = csub63(mont_mul<SP>(v, hp->P_R[i], m), m.q);
+    const u64 res = sub_mod(cq, vp, m.q);
+    o[i * N] = res;
+    if (p == 2) ext[((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k] = csub63(mont_mul<SP>(res, m.r2, m), m.q);
+  }
+}
+
 // CKKS rescale, the lift of the dropped limb (orc_rescale): x = INTT(c_{m})
 // in [0, q_m) becomes, for each remaining modulus q_i, [x]_{q_i} if
 // x <= q_m / 2, else [x - q_m]_{q_i} (the central lift OpenFHE's SwitchModulus
@@ -579,6 +708,29 @@ int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *d
   else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
   else hipLaunchKernelGGL((behz_floor_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
   return fhe_check(c, hipGetLastError(), "behz_floor");
+}
+
+template <bool SP>
+int hps_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
+  dim3 grid(c->n / EW_BLOCK, 4 * n);
+  const HpsDev *hp = (const HpsDev *)c->hps;
+  if (c->L == 8) hipLaunchKernelGGL((hps_extend_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
+  else if (c->L <= 8) hipLaunchKernelGGL((hps_extend_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
+  else if (c->L <= 16) hipLaunchKernelGGL((hps_extend_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
+  else hipLaunchKernelGGL((hps_extend_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
+  return fhe_check(c, hipGetLastError(), "hps_extend");
+}
+
+template <bool SP>
+int hps_scale_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+  dim3 grid(c->n / EW_BLOCK, n * 3);
+  const HpsDev *hp = (const HpsDev *)c->hps;
+  const u32 QP = c->L + c->K;
+  if (c->L == 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  else if (c->L <= 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  else if (c->L <= 16) hipLaunchKernelGGL((hps_scale_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  else hipLaunchKernelGGL((hps_scale_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  return fhe_check(c, hipGetLastError(), "hps_scale");
 }
 
 #define SP_DISPATCH(c, fn, ...) ((c)->special ? fn<true>(__VA_ARGS__) : fn<false>(__VA_ARGS__))
@@ -871,6 +1023,53 @@ int behz_setup(fhe_ctx *c) {
   return c->behz ? FHE_OK : FHE_ERR_OOM;
 }
 
+// HPS constants (oracle hps_init; the doubles by the same two C operations)
+int hps_setup(fhe_ctx *c) {
+  const u32 L = c->L, nB = c->nB, bsk0 = c->L + c->K;
+  if (L > BEHZ_MAXL) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "BFV with L > 24");
+  HpsDev *H = new HpsDev();
+  std::memset(H, 0, sizeof(HpsDev));
+  H->L = L; H->nB = nB; H->bsk0 = bsk0;
+  const u64 *qq = c->moduli.data(), *pp = c->moduli.data() + bsk0;
+  auto M = host_mulmod;
+  auto R = host_to_mont;
+  for (u32 i = 0; i < L; ++i) {
+    const u64 q = qq[i];
+    u64 h = 1;
+    for (u32 k = 0; k < L; ++k) if (k != i) h = M(h, qq[k] % q, q);
+    const u64 qt = host_inv(h, q), num = M(c->t % q, qt, q);
+    H->qt_R[i] = R(qt, q);
+    H->invq[i] = 1.0 / (double)q;
+    H->frac[i] = (double)num / (double)q;
+    H->ninv_R[i] = R(host_inv(c->n % q, q), q);
+    u64 Pm = 1;
+    for (u32 k = 0; k < nB; ++k) Pm = M(Pm, pp[k] % q, q);
+    H->P_R[i] = R(Pm, q);
+    for (u32 j = 0; j < nB; ++j) {
+      const u64 pj = pp[j];
+      u64 qs = 1, ps = 1;
+      for (u32 k = 0; k < L; ++k) if (k != i) qs = M(qs, qq[k] % pj, pj);
+      H->qstar_R[i][j] = R(qs, pj);
+      H->I_R[i][j] = R(M((pj - num % pj) % pj, host_inv(q % pj, pj), pj), pj);
+      for (u32 k = 0; k < nB; ++k) if (k != j) ps = M(ps, pp[k] % q, q);
+      H->pstar_R[j][i] = R(ps, q);
+    }
+  }
+  for (u32 j = 0; j < nB; ++j) {
+    const u64 pj = pp[j];
+    u64 Qm = 1, h = 1;
+    for (u32 k = 0; k < L; ++k) Qm = M(Qm, qq[k] % pj, pj);
+    H->Q_R[j] = R(Qm, pj);
+    H->lam_R[j] = R(M(M(c->t % pj, host_inv(Qm, pj), pj), host_inv(c->n % pj, pj), pj), pj);
+    for (u32 k = 0; k < nB; ++k) if (k != j) h = M(h, pp[k] % pj, pj);
+    H->pt_R[j] = R(host_inv(h, pj), pj);
+    H->invp[j] = 1.0 / (double)pj;
+  }
+  c->hps = ctx_upload(c, H, sizeof(HpsDev));
+  delete H;
+  return c->hps ? FHE_OK : FHE_ERR_OOM;
+}
+
 size_t bfv_mul_ws_bytes(const fhe_ctx *c, u32 n) {
   const size_t N = c->n, L = c->L, nB = c->nB;
   return sizeof(u64) * N * n * (4 * L + 4 * nB + 3 * L + 3 * nB) + keyswitch_ws_bytes(c, n);
@@ -886,8 +1085,10 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   u64 *eq = xb + (size_t)n * 4 * nB * N;      // [n][3][L][N]
   u64 *eb = eq + (size_t)n * 3 * L * N;       // [n][3][nB][N]
   const KsWs w = ks_layout(c, n, eb + (size_t)n * 3 * nB * N);
-  // 1-2. extend a0,a1,b0,b1 to Bsk (coefficient form)
-  if ((rc = SP_DISPATCH(c, behz_extend_impl, c, a, b, xb, n))) return rc;
+  // 1-2. extend a0,a1,b0,b1 to Bsk (coefficient form): BEHZ (m~ + sm_mrq) or
+  //      HPS (the exact centred lift, fhe_params.flags FHE_FLAG_BFV_HPS)
+  if ((rc = c->hps ? SP_DISPATCH(c, hps_extend_impl, c, a, b, xb, n) : SP_DISPATCH(c, behz_extend_impl, c, a, b, xb, n)))
+    return rc;
   // 3. NTT in Q and Bsk
   //    (the Q part out of place, straight from the ciphertexts)
   if ((rc = ntt_launch(c, LimbMap{xq, L, L, 0, L, 0, 0, 2 * n}, false, false, false, nullptr, a))) return rc;
@@ -900,7 +1101,10 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   if ((rc = ntt_inv_bfv_tensor_launch(c, xq, xq + (size_t)n * 2 * L * N, eq, L, 0, n))) return rc;
   if ((rc = ntt_inv_bfv_tensor_launch(c, xb, xb + (size_t)n * 2 * nB * N, eb, nB, bsk0, n))) return rc;
   // 5. scale and round: r0, r1 -> out; r2 -> the key-switch scratch, prepared
-  if ((rc = SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig))) return rc;
+  //    (BEHZ floor, or HPS simple scaling + exact P -> Q)
+  if ((rc = c->hps ? SP_DISPATCH(c, hps_scale_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig)
+                   : SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig)))
+    return rc;
   // 6. relinearize r2 and add to (r0, r1)
   return keyswitch_run(c, w, rlk, out, out, n, 3u, false);
 }

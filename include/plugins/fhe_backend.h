@@ -56,6 +56,14 @@ extern "C" {
 
 typedef struct fhe_ctx fhe_ctx;
 
+/* fhe_params.flags.  FHE_FLAG_BFV_HPS: BFV ct x ct multiplication by the HPS
+ * technique (Halevi-Polyakov-Shoup: exact centred base extension to the
+ * auxiliary base and simple scaling by t/Q with floating-point fractional
+ * parts; OpenFHE BFVrns multiplication technique HPS) instead of BEHZ (SEAL's
+ * RNSTool form, the default).  The two round differently, so their outputs
+ * differ bit for bit; both decrypt to m1*m2 mod t. */
+#define FHE_FLAG_BFV_HPS 1u
+
 typedef struct fhe_params {
   uint32_t scheme;         /* FHE_SCHEME_CKKS or FHE_SCHEME_BFV */
   uint32_t log_n;          /* ring degree N = 2^log_n, 10..17 */
@@ -64,7 +72,7 @@ typedef struct fhe_params {
   uint32_t dnum;           /* number of key-switching digits, alpha = ceil(L/dnum) */
   uint32_t q_bits;         /* bit size for generated Q primes (<= 61) */
   uint32_t p_bits;         /* bit size for generated P / Bsk primes (<= 61) */
-  uint32_t reserved;
+  uint32_t flags;          /* FHE_FLAG_*; 0 = defaults */
   uint64_t plain_modulus;  /* t (BFV only) */
   const uint64_t *moduli;  /* HOST pointer, optional explicit moduli in index-space order; NULL = generate */
 } fhe_params;

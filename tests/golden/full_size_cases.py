@@ -16,11 +16,13 @@ import numpy as np
 CKKS, BFV = 0, 1
 
 # name -> (scheme, log_n, L, K, dnum, t, op, n_ct, extra)
+# extra: the rotation steps (rotate), or "hps" for BFV mul_relin by HPS (else BEHZ)
 CASES = {
     "C1_bfv_add_n4096_l1": (BFV, 12, 1, 1, 1, 65537, "add", 4, None),
     "C2_ntt_fwd_n16384_l4": (CKKS, 14, 4, 0, 1, 0, "ntt_fwd", 2, None),
     "C2_ntt_inv_n16384_l4": (CKKS, 14, 4, 0, 1, 0, "ntt_inv", 2, None),
     "C3_bfv_mul_relin_n32768_l8": (BFV, 15, 8, 4, 2, 65537, "mul_relin", 1, None),
+    "C3_bfv_hps_mul_relin_n32768_l8": (BFV, 15, 8, 4, 2, 65537, "mul_relin", 1, "hps"),
     "C4_ckks_rotate_n65536_l12": (CKKS, 16, 12, 4, 3, 0, "rotate", 1, 1),
     "metric_ckks_mul_relin_n65536_l12": (CKKS, 16, 12, 4, 3, 0, "mul_relin", 1, None),
     "ckks_keyswitch_n65536_l12": (CKKS, 16, 12, 4, 3, 0, "keyswitch", 1, None),

@@ -45,7 +45,7 @@ def test_hip_matches_digests(name):
 
     hb.load_library()
     scheme, log_n, L, K, dnum, t, op, n_ct, extra = CASES[name]
-    c = hb.Context(scheme, log_n, L, K, dnum, t=t)
+    c = hb.Context(scheme, log_n, L, K, dnum, t=t, bfv_mult="hps" if extra == "hps" else "behz")
     assert [int(q) for q in c.moduli] == DIGESTS[name]["moduli"]
     sh = shapes(CASES[name])
     a = c.fill_uniform(hb.empty(sh["a"]), seed=SEED_A)

@@ -686,3 +686,77 @@ def test_base_conv_contexts_recreated(hb):
         torch.cuda.synchronize()
         assert np.array_equal(hb.to_host(y), o.base_conv(x, src, dst)), (log_n, bits)
         c.close()
+
+
+# ------------------------------------------------------------------ BFV HPS
+def hps_pair(hb, log_n, L, K, dnum, t=65537, moduli=None):
+    o = Oracle(SCHEME_BFV, log_n, L, K, dnum, t=t, moduli=moduli, bfv_mult="hps")
+    g = hb.Context(SCHEME_BFV, log_n, L, K, dnum, t=t, moduli=o.moduli, bfv_mult="hps")
+    assert np.array_equal(g.moduli, o.moduli)
+    return o, g
+
+
+def test_bfv_hps_golden(hb):
+    """HPS multiplication against the big-int model's restatement (its float
+    parts included; the model checks round(t d / Q) on integers)."""
+    g = load("bfv_hps_n1024_l4.npz")
+    o, c = hps_pair(hb, 10, 4, 2, 2, t=int(g["t"]), moduli=g["moduli"])
+    out = hb.empty((1, 2, 4, 1 << 10))
+    c.mul_relin(hb.to_device(g["a"][None]), hb.to_device(g["b"][None]), hb.to_device(g["rlk"]), out)
+    assert np.array_equal(hb.to_host(out)[0], g["out_mul"])
+
+
+@pytest.mark.parametrize("log_n,L,K,dnum,n_ct", [(15, 8, 4, 2, 2), (13, 5, 2, 3, 3), (12, 11, 3, 4, 1)])
+def test_bfv_hps_mul_relin_vs_oracle(hb, log_n, L, K, dnum, n_ct):
+    """(15, 8, 4, 2) is BASELINE C3; L = 5 and 11 take the non-exact-L kernels."""
+    o, c = hps_pair(hb, log_n, L, K, dnum)
+    a = o.uniform((n_ct, 2, L, 1 << log_n), seed=61)
+    b = o.uniform((n_ct, 2, L, 1 << log_n), seed=62)
+    rlk = o.uniform(o.key_shape(), seed=63)
+    want = o.mul_relin(a, b, rlk)
+    dout = hb.empty(a.shape)
+    c.mul_relin(hb.to_device(a), hb.to_device(b), hb.to_device(rlk), dout)
+    assert np.array_equal(hb.to_host(dout), want)
+
+
+def test_bfv_hps_edge_values(hb):
+    """All-zero, all q-1 and mixed extreme residues (the float sums at their ends)."""
+    o, c = hps_pair(hb, 13, 3, 2, 2)
+    n = o.n
+    qs = o.moduli[:3][None, None, :, None]
+    a = np.broadcast_to(qs - 1, (1, 2, 3, n)).astype(np.uint64).copy()
+    b = np.zeros((1, 2, 3, n), dtype=np.uint64)
+    b[..., ::2] = 1
+    b[..., 1::3] = (qs - 1).reshape(1, 1, 3, 1)
+    rlk = o.uniform(o.key_shape(), seed=64)
+    for x, y in ((a, a), (a, b), (b, b), (np.zeros_like(a), a)):
+        want = o.mul_relin(x, y, rlk)
+        dout = hb.empty(x.shape)
+        c.mul_relin(hb.to_device(x), hb.to_device(y), hb.to_device(rlk), dout)
+        assert np.array_equal(hb.to_host(dout), want)
+
+
+def test_bfv_hps_real_keys_exact(hb):
+    """Dec(Mul+Relin(Enc m1, Enc m2)) = m1 m2 mod t with HPS at C3's ring size."""
+    t = 65537
+    o, c = hps_pair(hb, 15, 8, 4, 2, t=t)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    Qp = math.prod(Q)
+    s = o.secret(18)
+    s_qp = o.signed_to_rns(s, 0, o.L + o.K, ntt=True)
+    qs = o.moduli[:o.L + o.K].astype(object)[:, None]
+    sq = ((s_qp.astype(object) * s_qp.astype(object)) % qs).astype(np.uint64)
+    rlk = o.switch_key(sq, s_qp, seed=19)
+    rng = random.Random(20)
+    m1 = [0] * o.n
+    for k in rng.sample(range(o.n), 40):
+        m1[k] = rng.randrange(t)
+    m2 = [rng.randrange(t) for _ in range(o.n)]
+    delta = Qp // t
+    c1 = o.encrypt(to_rns([delta * x for x in m1], Q), s_qp, 21)
+    c2 = o.encrypt(to_rns([delta * x for x in m2], Q), s_qp, 22)
+    dout = hb.empty((1, 2, o.L, o.n))
+    c.mul_relin(hb.to_device(c1[None]), hb.to_device(c2[None]), hb.to_device(rlk), dout)
+    v = crt_centered(o.decrypt(hb.to_host(dout)[0], s_qp), Q)
+    dec = [((t * x + Qp // 2) // Qp) % t for x in v]
+    assert dec == [x % t for x in negacyclic_int(m1, m2)]
