@@ -36,8 +36,11 @@ Extra fields:
                   a bounded sample of the same workload, in a child process on
                   the host's cores (rank 0, N=1 only); also C2/C3/C4 samples.
   secondary    -- per-GPU throughput of the other BASELINE configs (C4 rotate,
-                  C3 BFV mul+relin, C2 NTT) and the metric config on
-                  OpenFHE-style primes (generic Montgomery path).
+                  C3 BFV mul+relin by BEHZ and by HPS, C2 NTT) and the metric
+                  config on OpenFHE-style primes (generic Montgomery path).
+  step         -- the headline op's own roofline: rocprofv3-counted HBM bytes per
+                  ct-mult (profiles/step_traffic.json), the fraction of peak the
+                  measured rate moves with them, the dominant kernel of a wave.
 """
 from __future__ import annotations
 
@@ -581,8 +584,13 @@ def secondary_configs(hb, ctx, gk, a, b, out, dev, stream, B, reps):
     o3 = hb.empty((B, 2, 8, n3), device=dev)
     t = _timed(lambda: bfv.mul_relin(a3, b3, k3, o3), reps, stream)
     res["C3_bfv_mul_relin_per_s"] = round(B / t, 1)
-    del a3, b3, k3, o3
     bfv.close()
+    hps = hb.Context(hb.SCHEME_BFV, 15, 8, 4, 2, t=65537, device=dev.index, bfv_mult="hps")
+    hps.set_stream(stream)
+    t = _timed(lambda: hps.mul_relin(a3, b3, k3, o3), reps, stream)
+    res["C3_bfv_hps_mul_relin_per_s"] = round(B / t, 1)
+    del a3, b3, k3, o3
+    hps.close()
     c2 = hb.Context(hb.SCHEME_CKKS, 14, 4, device=dev.index)
     c2.set_stream(stream)
     polys = 256

@@ -211,15 +211,19 @@ __device__ __forceinline__ u64 ld_d(const u64 *base, u32 off) {
 }
 __device__ __forceinline__ void st_b(u64 *base, u32 off, u64 v) { *(u64 *)((char *)base + off) = v; }
 
+#ifndef LDS_PAD
+#define LDS_PAD 1  // 0: unpadded exchange tile (32 KiB at S = 8, W = 16: 5 workgroups per CU, bank conflicts)
+#endif
+__host__ __device__ constexpr u32 lds_pad(u32 k) { return LDS_PAD ? (k >> 4) : 0; }
 template <int S>
 __device__ __forceinline__ u32 lds_idx(u32 w, u32 k) {
   constexpr u32 SUB = 1u << S;
-  constexpr u32 PAD = SUB + (SUB >> 4) + 1;
-  return w * PAD + k + (k >> 4);
+  constexpr u32 PAD = SUB + (LDS_PAD ? (SUB >> 4) + 1 : 0);
+  return w * PAD + k + lds_pad(k);
 }
 template <int S, int W>
 constexpr size_t lds_bytes() {
-  return (size_t)W * ((1u << S) + (1u << S >> 4) + 1) * sizeof(u64);
+  return (size_t)W * ((1u << S) + (LDS_PAD ? (1u << S >> 4) + 1 : 0)) * sizeof(u64);
 }
 
 
@@ -395,13 +399,13 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
     const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + (GP::k_reg(r) >> 4)] = x[r];
+    for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + lds_pad(GP::k_reg(r))] = x[r];
     __syncthreads();
     const u32 lr = lds_idx<S>(w, Grp<S, LOGR, GN>::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const u32 kr = Grp<S, LOGR, GN>::k_reg(r);
-      x[r] = lds[lr + kr + (kr >> 4)];
+      x[r] = lds[lr + kr + lds_pad(kr)];
     }
     group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, GI + 1>(x, tn, lds, tw, data, voff, w, ts, hi, a, mi,
                                                                      mod, ep);
@@ -481,14 +485,14 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
       // re-layout through LDS so the HBM store is coalesced (group-0 layout)
       const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
 #pragma unroll
-      for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + (GP::k_reg(r) >> 4)] = x[r];
+      for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + lds_pad(GP::k_reg(r))] = x[r];
       __syncthreads();
       using G0 = Grp<S, LOGR, 0>;
       const u32 lr = lds_idx<S>(w, G0::k_thr(ts));
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const u32 kr = G0::k_reg(r);
-        const u64 v = lds[lr + kr + (kr >> 4)];
+        const u64 v = lds[lr + kr + lds_pad(kr)];
         if constexpr (is_combine(EPI)) {
           // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM.
           // acc - conv is formed as acc + Bq - v (v < Bq, B = 4 WIDE / 2): below
@@ -702,14 +706,14 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
     }
     const u32 lw = lds_idx<S>(w, GZ::k_thr(ts));
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[lw + GZ::k_reg(r) + (GZ::k_reg(r) >> 4)] = x[r];
+    for (int r = 0; r < R; ++r) lds[lw + GZ::k_reg(r) + lds_pad(GZ::k_reg(r))] = x[r];
     __syncthreads();
     using GF = Grp<S, LOGR, G0>;
     const u32 lr = lds_idx<S>(w, GF::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const u32 kr = GF::k_reg(r);
-      x[r] = lds[lr + kr + (kr >> 4)];
+      x[r] = lds[lr + kr + lds_pad(kr)];
     }
   } else {
     using GF = Grp<S, LOGR, G0>;
