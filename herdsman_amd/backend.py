@@ -84,6 +84,8 @@ SIGNATURES = {
     "fhe_rotate_at": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _u32, _u32]),
     "fhe_keyswitch_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
     "fhe_rescale": (C.c_int, [_vp, _vp, _vp, _u32, _u32]),
+    "fhe_level_reduce": (C.c_int, [_vp, _vp, _vp, _u32, _u32, _u32]),
+    "fhe_reduce_at": (C.c_int, [_vp, _vp, _u32, C.c_int, _vp, _vp, _u32]),
     "fhe_reduce": (C.c_int, [_vp, _vp, _u32, C.c_int, _vp, _vp]),
     "fhe_bcast_key": (C.c_int, [_vp, _vp, _sz, _vp, C.c_int]),
     "fhe_reduce_ranks": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, C.c_int, _vp]),
@@ -351,6 +353,13 @@ class Context:
         if out.shape[0] != ct.shape[0]:
             raise FheBackendError("rescale: input and output batch sizes differ")
         self._ck(self.lib.fhe_rescale(self.h, _ptr(ct), _ptr(out), n, level), "fhe_rescale")
+        return out
+
+    def level_reduce(self, ct, out, level_in: int, level_out: int):
+        """Drop the Q limbs past level_out (no scaling)."""
+        n = self._ct_level(level_in, ct)
+        self._ct_level(level_out, out)
+        self._ck(self.lib.fhe_level_reduce(self.h, _ptr(ct), _ptr(out), n, level_in, level_out), "fhe_level_reduce")
         return out
 
     def reduce(self, cts, op: int, rlk=None, out=None):

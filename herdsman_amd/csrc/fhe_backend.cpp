@@ -725,6 +725,24 @@ int fhe_rescale(fhe_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, ui
   return FHE_OK;
 }
 
+int fhe_level_reduce(fhe_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t level_in,
+                     uint32_t level_out) {
+  if (!c) return FHE_ERR_INVALID;
+  if (c->params.scheme != FHE_SCHEME_CKKS) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "level reduce is CKKS only");
+  if (level_in > c->L || level_out == 0 || level_out >= level_in)
+    return fhe_fail(c, FHE_ERR_INVALID, "level reduce needs 1 <= level_out < level_in <= L");
+  if (!n_ct) return FHE_OK;
+  if (!ct || !out) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
+  const size_t N = c->n, in_w = (size_t)2 * level_in * N, out_w = (size_t)2 * level_out * N;
+  if (!(out + n_ct * out_w <= ct || ct + n_ct * in_w <= out))
+    return fhe_fail(c, FHE_ERR_INVALID, "level reduce output overlaps its input");
+  DeviceBind bind(c);
+  // one strided copy: 2 n_ct rows of level_out limbs, source pitch level_in limbs
+  return fhe_check(c, hipMemcpy2DAsync(out, level_out * N * 8, ct, level_in * N * 8, level_out * N * 8,
+                                       (size_t)2 * n_ct, hipMemcpyDeviceToDevice, c->stream),
+                   "level reduce");
+}
+
 int fhe_galois_elt(const fhe_ctx *c, int32_t steps, uint32_t *out) {
   if (!c || !out) return FHE_ERR_INVALID;
   const int64_t ord = c->n / 2;
@@ -754,6 +772,14 @@ int fhe_reduce(fhe_ctx *c, uint64_t *cts, uint32_t n_ct, int op, const uint64_t 
   }
   if (out != cts) return fhe_check(c, hipMemcpyAsync(out, cts, cw * 8, hipMemcpyDeviceToDevice, c->stream), "copy");
   return FHE_OK;
+}
+
+int fhe_reduce_at(fhe_ctx *c, uint64_t *cts, uint32_t n_ct, int op, const uint64_t *rlk, uint64_t *out,
+                  uint32_t level) {
+  fhe_ctx *v;
+  DeviceBind bind(c);
+  int rc = at_level(c, level, &v);
+  return rc ? rc : from_view(c, v, fhe_reduce(v, cts, n_ct, op, rlk, out));
 }
 
 int fhe_reduce_schedule(int rank, int world, int root, int32_t *steps, int cap) {

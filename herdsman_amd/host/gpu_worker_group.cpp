@@ -276,7 +276,9 @@ struct SchemaCtx {
   uint32_t scheme = 0, log_n = 0, L = 0, K = 0, dnum = 0;
   std::vector<uint64_t> moduli;
   uint64_t q_digest = 0, qp_digest = 0;
-  size_t ct_words() const { return (size_t)2 * L << log_n; }
+  std::vector<uint64_t> level_digest;  // [m] = digest of the first m Q moduli (a level-m ciphertext's header)
+  size_t ct_words(uint32_t level) const { return (size_t)2 * level << log_n; }
+  size_t ct_words() const { return ct_words(L); }
   size_t key_words() const { return (size_t)dnum * 2 * (L + K) << log_n; }
 };
 
@@ -369,6 +371,7 @@ struct Slot {
   std::vector<std::unique_ptr<Pinned>> in;
   Pinned out;
   size_t r0 = 0, n = 0;
+  uint32_t out_level = 0;  // level of the batch's result ciphertexts
 };
 
 // one lane's state for one schema: context (own stream), buffers, staging
@@ -535,7 +538,7 @@ void GpuWorkerGroup::completion_loop() {
 // ------------------------------------------------------------- evaluation
 namespace {
 
-enum class Op : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4 };
+enum class Op : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4, RESCALE = 5 };
 struct Instr {
   Op op;
   int32_t arg;
@@ -552,7 +555,7 @@ std::vector<Instr> lower_circuit(const C &c) {
     std::vector<Instr> out;
     for (const auto &i : c.program) {
       const uint32_t op = static_cast<uint32_t>(i.op);
-      if (op > static_cast<uint32_t>(Op::ROTATE)) throw std::runtime_error("unknown circuit op");
+      if (op > static_cast<uint32_t>(Op::RESCALE)) throw std::runtime_error("unknown circuit op");
       out.push_back(Instr{static_cast<Op>(op), static_cast<int32_t>(i.arg)});
     }
     return out;
@@ -598,6 +601,8 @@ LaneSchema &lane_schema(std::map<int, std::unique_ptr<LaneSchema>> &m, const Gpu
   fhe_ctx_moduli(s.ctx, s.moduli.data(), cnt, nullptr);
   s.q_digest = moduli_digest(s.moduli.data(), s.L);
   s.qp_digest = moduli_digest(s.moduli.data(), s.L + s.K);
+  s.level_digest.resize(s.L + 1);
+  for (uint32_t m = 1; m <= s.L; ++m) s.level_digest[m] = moduli_digest(s.moduli.data(), m);
   auto &slot = m[schema];
   slot = std::move(ls);
   // the lane's own stream: lanes of one device run concurrently
@@ -640,19 +645,22 @@ std::shared_ptr<KeySet> device_keys(std::mutex &m, std::map<std::pair<std::strin
   return k;
 }
 
-void check_ct_header(const SchemaCtx &s, const CtHeader &h) {
-  if (h.magic != kCtMagic || h.version != 1 || h.scheme != s.scheme || h.log_n != s.log_n || h.n_limbs != s.L ||
-      h.moduli_digest != s.q_digest)
+// the ciphertext's level (its limb count): 1..L for CKKS, L for BFV
+uint32_t check_ct_header(const SchemaCtx &s, const CtHeader &h) {
+  const bool level_ok = s.scheme == FHE_SCHEME_CKKS ? (h.n_limbs >= 1 && h.n_limbs <= s.L) : h.n_limbs == s.L;
+  if (h.magic != kCtMagic || h.version != 1 || h.scheme != s.scheme || h.log_n != s.log_n || !level_ok ||
+      h.moduli_digest != s.level_digest[h.n_limbs])
     throw std::runtime_error("ciphertext header does not match the schema context");
+  return h.n_limbs;
 }
 
-CtHeader ct_header(const SchemaCtx &s) {
+CtHeader ct_header(const SchemaCtx &s, uint32_t level) {
   CtHeader h;
   h.scheme = (uint8_t)s.scheme;
   h.domain = s.scheme == FHE_SCHEME_CKKS ? 1 : 0;
   h.log_n = s.log_n;
-  h.n_limbs = s.L;
-  h.moduli_digest = s.q_digest;
+  h.n_limbs = level;
+  h.moduli_digest = s.level_digest[level];
   return h;
 }
 
@@ -667,32 +675,69 @@ const DevBuf &galois_key(const SchemaCtx &s, const KeySet &ks, int32_t steps, ui
 // the partition file into slot k % 2's pinned buffers (pread), then enqueue
 // H2D, the program's ops and D2H on the lane's stream and mark the slot.
 // Nothing waits for the GPU here.
+// One operand of the stack program: a batch of n ciphertexts at one level.
+struct StackCt {
+  ArenaBuf buf;
+  uint32_t level = 0;
+};
+
+// The level-m copy of a (the first m limbs of each poly), or a itself
+StackCt at_level(LaneSchema &ls, StackCt a, uint32_t m, size_t n) {
+  if (a.level == m) return a;
+  const SchemaCtx &s = ls.s;
+  StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
+  ck(s.ctx, fhe_level_reduce(s.ctx, a.buf.p, o.buf.p, (uint32_t)n, a.level, m), "level_reduce");
+  return o;
+}
+
+// Batch k of a MapTask, first half: read the rows' ciphertexts straight from
+// the partition file into slot k % 2's pinned buffers (pread), then enqueue
+// H2D, the program's ops and D2H on the lane's stream and mark the slot.
+// Nothing waits for the GPU here.  A row holds its ciphertexts back to back,
+// each CtHeader + 2 m N words at its own level m (CKKS); the batch's first
+// row fixes each input's level, and every row must match it.
 void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vector<Instr> &prog,
                        const PartitionIndex &rows, size_t r0, size_t n, unsigned io_threads, StageStats &st) {
   const SchemaCtx &s = ls.s;
   Slot &sl = ls.slot[si];
   sl.r0 = r0;
   sl.n = n;
-  const size_t cw = s.ct_words(), one = sizeof(CtHeader) + cw * 8;
-  std::vector<ArenaBuf> stack;
+  // byte offset and level of every input index the program pushes
+  int32_t max_in = -1;
+  for (const auto &ins : prog)
+    if (ins.op == Op::PUSH_INPUT) max_in = std::max(max_in, ins.arg);
+  std::vector<size_t> in_off;
+  std::vector<uint32_t> in_level;
+  for (size_t off = 0; (int32_t)in_off.size() <= max_in;) {
+    CtHeader h;
+    rows.read(r0, off, &h, sizeof(h));
+    const uint32_t m = check_ct_header(s, h);
+    in_off.push_back(off);
+    in_level.push_back(m);
+    off += sizeof(h) + s.ct_words(m) * 8;
+  }
+  std::vector<StackCt> stack;
   size_t push = 0;
   double read_s = 0;
   const auto t_enq = std::chrono::steady_clock::now();
   for (const auto &ins : prog) {
     switch (ins.op) {
       case Op::PUSH_INPUT: {
+        if (ins.arg < 0) throw std::runtime_error("negative input index");
+        const uint32_t m = in_level[ins.arg];
+        const size_t cw = s.ct_words(m), off = in_off[ins.arg];
         if (sl.in.size() <= push) sl.in.push_back(std::make_unique<Pinned>());
         uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[push++]->reserve(s.ctx, cw * n * 8));
         const auto t_r = std::chrono::steady_clock::now();
         parallel_for(n, io_threads, [&](size_t r) {
           CtHeader h;
-          rows.read(r0 + r, (size_t)ins.arg * one, &h, sizeof(h));
-          check_ct_header(s, h);
-          rows.read(r0 + r, (size_t)ins.arg * one + sizeof(h), host + r * cw, cw * 8);
+          rows.read(r0 + r, off, &h, sizeof(h));
+          if (check_ct_header(s, h) != m) throw std::runtime_error("rows of a batch differ in ciphertext level");
+          rows.read(r0 + r, off + sizeof(h), host + r * cw, cw * 8);
         });
         read_s += secs_since(t_r);
-        ArenaBuf d(*ls.arena, cw * n);
-        ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, d.p, host, cw * n * 8), "h2d");
+        StackCt d{ArenaBuf(*ls.arena, cw * n), m};
+        ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, d.buf.p, host, cw * n * 8), "h2d");
         stack.push_back(std::move(d));
         break;
       }
@@ -700,16 +745,19 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
       case Op::SUB:
       case Op::MUL_RELIN: {
         if (stack.size() < 2) throw std::runtime_error("circuit stack underflow");
-        ArenaBuf b = std::move(stack.back());
+        StackCt b = std::move(stack.back());
         stack.pop_back();
-        ArenaBuf a = std::move(stack.back());
+        StackCt a = std::move(stack.back());
         stack.pop_back();
-        ArenaBuf o(*ls.arena, cw * n);
-        if (ins.op == Op::ADD) ck(s.ctx, fhe_add(s.ctx, a.p, b.p, o.p, (uint32_t)n), "add");
-        else if (ins.op == Op::SUB) ck(s.ctx, fhe_sub(s.ctx, a.p, b.p, o.p, (uint32_t)n), "sub");
+        const uint32_t m = std::min(a.level, b.level);
+        a = at_level(ls, std::move(a), m, n);
+        b = at_level(ls, std::move(b), m, n);
+        StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
+        if (ins.op == Op::ADD) ck(s.ctx, fhe_add_at(s.ctx, a.buf.p, b.buf.p, o.buf.p, (uint32_t)n, m), "add");
+        else if (ins.op == Op::SUB) ck(s.ctx, fhe_sub_at(s.ctx, a.buf.p, b.buf.p, o.buf.p, (uint32_t)n, m), "sub");
         else {
           if (!ks.relin.p) throw std::runtime_error("no relinearisation key");
-          ck(s.ctx, fhe_mul_relin(s.ctx, a.p, b.p, ks.relin.p, o.p, (uint32_t)n), "mul_relin");
+          ck(s.ctx, fhe_mul_relin_at(s.ctx, a.buf.p, b.buf.p, ks.relin.p, o.buf.p, (uint32_t)n, m), "mul_relin");
         }
         stack.push_back(std::move(o));
         break;
@@ -718,8 +766,18 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
         if (stack.empty()) throw std::runtime_error("circuit stack underflow");
         uint32_t g = 0;
         const DevBuf &gk = galois_key(s, ks, ins.arg, &g);
-        ArenaBuf o(*ls.arena, cw * n);
-        ck(s.ctx, fhe_rotate(s.ctx, stack.back().p, g, gk.p, o.p, (uint32_t)n), "rotate");
+        const uint32_t m = stack.back().level;
+        StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
+        ck(s.ctx, fhe_rotate_at(s.ctx, stack.back().buf.p, g, gk.p, o.buf.p, (uint32_t)n, m), "rotate");
+        stack.back() = std::move(o);
+        break;
+      }
+      case Op::RESCALE: {
+        if (stack.empty()) throw std::runtime_error("circuit stack underflow");
+        const uint32_t m = stack.back().level;
+        if (m < 2) throw std::runtime_error("rescale of a level-1 ciphertext");
+        StackCt o{ArenaBuf(*ls.arena, s.ct_words(m - 1) * n), m - 1};
+        ck(s.ctx, fhe_rescale(s.ctx, stack.back().buf.p, o.buf.p, (uint32_t)n, m), "rescale");
         stack.back() = std::move(o);
         break;
       }
@@ -728,8 +786,10 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
     }
   }
   if (stack.size() != 1) throw std::runtime_error("circuit must leave exactly one ciphertext");
+  sl.out_level = stack.back().level;
+  const size_t cw = s.ct_words(sl.out_level);
   uint64_t *host = reinterpret_cast<uint64_t *>(sl.out.reserve(s.ctx, cw * n * 8));
-  ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, host, stack.back().p, cw * n * 8), "d2h");
+  ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, host, stack.back().buf.p, cw * n * 8), "d2h");
   // the device buffers go back to the arena now: later ops that reuse them are
   // ordered after this batch's copies by the stream
   ck(s.ctx, fhe_mark(s.ctx, (uint32_t)si), "mark");
@@ -746,9 +806,9 @@ void finish_map_batch(LaneSchema &ls, int si, PartitionWriter &out, unsigned io_
   ck(s.ctx, fhe_wait_mark(s.ctx, (uint32_t)si), "batch wait");
   st.wait_s += secs_since(t0);
   t0 = std::chrono::steady_clock::now();
-  const size_t cw = s.ct_words();
+  const size_t cw = s.ct_words(sl.out_level);
   const uint64_t *host = reinterpret_cast<const uint64_t *>(sl.out.p);
-  const CtHeader h = ct_header(s);
+  const CtHeader h = ct_header(s, sl.out_level);
   const uint64_t row_bytes = 4 + sizeof(h) + cw * 8;
   const uint64_t base = out.claim(row_bytes * sl.n);
   parallel_for(sl.n, io_threads,
@@ -825,8 +885,18 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
           count += parts.back()->size();
         }
         if (count == 0) throw std::runtime_error("reduce over no rows");
-        const size_t cw = s.ct_words();
+        // every row's first ciphertext, all at one level (the first row's)
+        uint32_t level = 0;
+        for (const auto &pv : parts)
+          if (pv->size()) {
+            CtHeader h;
+            pv->read(0, 0, &h, sizeof(h));
+            level = check_ct_header(s, h);
+            break;
+          }
+        const size_t cw = s.ct_words(level);
         Slot &sl = ls.slot[0];
+        sl.out_level = level;
         if (sl.in.empty()) sl.in.push_back(std::make_unique<Pinned>());
         uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[0]->reserve(s.ctx, count * cw * 8));
         size_t r = 0;
@@ -834,20 +904,20 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
           for (size_t i = 0; i < pv->size(); ++i, ++r) {
             CtHeader h;
             pv->read(i, 0, &h, sizeof(h));
-            check_ct_header(s, h);
+            if (check_ct_header(s, h) != level) throw std::runtime_error("reduce inputs differ in ciphertext level");
             pv->read(i, sizeof(h), host + r * cw, cw * 8);
           }
         ArenaBuf a(*ls.arena, count * cw);
         ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, a.p, host, count * cw * 8), "h2d");
         // balanced tree, one batched add / mul+relin per level (fhe_reduce)
-        ck(s.ctx, fhe_reduce(s.ctx, a.p, (uint32_t)count, mul ? FHE_REDUCE_MUL_RELIN : FHE_REDUCE_ADD,
-                             mul ? ks->relin.p : nullptr, a.p), "reduce");
+        ck(s.ctx, fhe_reduce_at(s.ctx, a.p, (uint32_t)count, mul ? FHE_REDUCE_MUL_RELIN : FHE_REDUCE_ADD,
+                                mul ? ks->relin.p : nullptr, a.p, level), "reduce");
         uint64_t *res = reinterpret_cast<uint64_t *>(sl.out.reserve(s.ctx, cw * 8));
         ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, res, a.p, cw * 8), "d2h");
         ck(s.ctx, fhe_synchronize(s.ctx), "reduce sync");
         PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr),
                             config_.durable_outputs);
-        const CtHeader h = ct_header(s);
+        const CtHeader h = ct_header(s, level);
         out.append({{&h, sizeof(h)}, {res, cw * 8}});
         out.commit();
       }

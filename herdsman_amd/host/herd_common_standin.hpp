@@ -53,7 +53,9 @@ struct CryptoKeyPtr {
 };
 
 // Stand-in circuit: a stack program over the ciphertexts of one row.
-enum class CtOp : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4 };
+// CKKS operands may sit at different levels: binary ops run at the lower one
+// (the other operand's extra limbs dropped), RESCALE drops one level.
+enum class CtOp : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4, RESCALE = 5 };
 struct CircuitInstr {
   CtOp op;
   int32_t arg = 0;  // PUSH_INPUT: index of the ciphertext in the row; ROTATE: steps

@@ -15,7 +15,7 @@
 //                 (partition read, PCIe both ways, GPU, partition write): the
 //                 mean and spread of REPS (default 5) warm repetitions after one
 //                 warm-up, and where the lanes' time went (GpuWorkerGroup::stage_stats).
-// PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file]   PROGRAM tokens: in<i> add sub mul rot:<k>
+// PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file]   PROGRAM tokens: in<i> add sub mul rot:<k> rescale
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -79,6 +79,7 @@ static herd::common::Circuit parse_program(int argc, char **argv, int first) {
     else if (t == "sub") c.program.push_back({CtOp::SUB, 0});
     else if (t == "mul") c.program.push_back({CtOp::MUL_RELIN, 0});
     else if (t.rfind("rot:", 0) == 0) c.program.push_back({CtOp::ROTATE, std::stoi(t.substr(4))});
+    else if (t == "rescale") c.program.push_back({CtOp::RESCALE, 0});
     else throw std::runtime_error("unknown program token " + t);
   }
   return c;

@@ -168,6 +168,14 @@ int fhe_keyswitch_at(fhe_ctx *ctx, const uint64_t *d, const uint64_t *ksk, uint6
  * SEAL divide_and_round_q_last_ntt (the dropped limb lifted centrally).
  * out must not overlap ct. */
 int fhe_rescale(fhe_ctx *ctx, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t level);
+/* level_out < level_in: drop the Q limbs past level_out without scaling (OpenFHE
+ * LevelReduce): out [n_ct][2][level_out][N] = the first level_out limbs of each
+ * poly of ct [n_ct][2][level_in][N].  out must not overlap ct. */
+int fhe_level_reduce(fhe_ctx *ctx, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t level_in,
+                     uint32_t level_out);
+/* fhe_reduce on ciphertexts of level `level` (cts, out [.][2][level][N]) */
+int fhe_reduce_at(fhe_ctx *ctx, uint64_t *cts, uint32_t n_ct, int op, const uint64_t *rlk, uint64_t *out,
+                  uint32_t level);
 
 /* ---- reductions ---------------------------------------
  * Homomorphic reduction of n_ct ciphertexts to one, the evaluation of one

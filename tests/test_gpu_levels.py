@@ -187,3 +187,27 @@ def test_depth3_real_keys(hb, metric):
     assert abs(dec[0] - want) < 2 ** 32, (dec[0], float(want))
     assert max(abs(v) for v in dec[1:]) < 2 ** 32
     assert abs(want) > 2 ** 56  # the message is far above the noise (2^32)
+
+
+def test_level_reduce_and_reduce_at(hb, metric):
+    """fhe_level_reduce keeps the first limbs of every poly; fhe_reduce_at runs
+    the balanced tree on a level view (add and mul+relin)."""
+    o, c = metric
+    ct = o.uniform((3, 2, 9, o.n), seed=800)
+    out = hb.empty((3, 2, 5, o.n))
+    c.level_reduce(hb.to_device(ct), out, 9, 5)
+    assert np.array_equal(hb.to_host(out), ct[:, :, :5])
+    lvl = 6
+    cts = o.uniform((5, 2, lvl, o.n), seed=801)
+    k = o.uniform(o.key_shape(), seed=802)
+    lib = hb.load_library()
+    d = hb.to_device(cts)
+    res = hb.empty((1, 2, lvl, o.n))
+    assert lib.fhe_reduce_at(c.h, hb._ptr(d), 5, hb.REDUCE_MUL_RELIN, hb._ptr(hb.to_device(k)), hb._ptr(res),
+                             lvl) == 0
+    live = list(cts)
+    while len(live) > 1:
+        half = len(live) // 2
+        comb = o.mul_relin_at(np.stack(live[:half]), np.stack(live[len(live) - half:]), k, lvl)
+        live = list(comb) + live[half:len(live) - half]
+    assert np.array_equal(hb.to_host(res)[0], live[0])

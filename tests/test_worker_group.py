@@ -40,18 +40,23 @@ def fnv(moduli):
 
 
 def ct_row(o, cts):
-    """row payload: concatenated (CtHeader + words) ciphertexts."""
+    """row payload: concatenated (CtHeader + words) ciphertexts, each at its own
+    level (its limb count, CKKS)."""
     out = b""
     for ct in cts:
-        hdr = struct.pack("<IHBBIIQ", 0x54434648, 1, o.scheme, 1 if o.scheme == 0 else 0, o.log_n, o.L,
-                          fnv(o.moduli[:o.L]))
+        lvl = ct.shape[-2]
+        hdr = struct.pack("<IHBBIIQ", 0x54434648, 1, o.scheme, 1 if o.scheme == 0 else 0, o.log_n, lvl,
+                          fnv(o.moduli[:lvl]))
         out += hdr + np.ascontiguousarray(ct, dtype=np.uint64).tobytes()
     return out
 
 
-def parse_row(o, payload):
+def parse_row(o, payload, level=None):
     assert struct.unpack_from("<I", payload)[0] == 0x54434648
-    return np.frombuffer(payload[24:], dtype=np.uint64).reshape(2, o.L, o.n)
+    lvl = struct.unpack_from("<I", payload, 12)[0]
+    assert lvl == (o.L if level is None else level)
+    assert struct.unpack_from("<Q", payload, 16)[0] == fnv(o.moduli[:lvl])
+    return np.frombuffer(payload[24:], dtype=np.uint64).reshape(2, lvl, o.n)
 
 
 def write_partition(path, rows):
@@ -159,6 +164,33 @@ def test_gpu_map_task_mul_rotate(wg_run, tmp_path):
     got = np.stack([parse_row(o, p) for p in read_partition(os.path.join(storage, "sess", "frameB", "2"))])
     want = o.rotate(o.mul_relin(a, b, rlk), g, gk)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_map_task_ckks_levels(wg_run, tmp_path):
+    """A depth-2 CKKS circuit through the worker group: rows carry ciphertexts at
+    levels 12, 12 and 11; in0 in1 mul rescale in1 mul in2 add rescale runs the
+    second product at level 11 (in1's 12th limb dropped), adds the level-11
+    input and writes level-10 rows, bit-exact vs the oracle's level ops."""
+    from oracle_ffi import SCHEME_CKKS
+    o, storage, keys = _setup(tmp_path, SCHEME_CKKS, 16, 12, 4, 3)
+    rows = 2
+    a = o.uniform((rows, 2, 12, o.n), seed=31)
+    b = o.uniform((rows, 2, 12, o.n), seed=32)
+    c = o.uniform((rows, 2, 11, o.n), seed=33)
+    rlk = o.uniform(o.key_shape(), seed=34)
+    write_partition(os.path.join(storage, "sl", "fa", "0"), [ct_row(o, [a[i], b[i], c[i]]) for i in range(rows)])
+    write_keys(os.path.join(keys, "sl", "0.key"), o, rlk, {})
+    r = subprocess.run([wg_run, "map", storage, keys, "sl", "0", params_arg(o, str(tmp_path)), "fa", "0", "fb",
+                        "in0", "in1", "mul", "rescale", "in1", "mul", "in2", "add", "rescale"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.stack([parse_row(o, p, level=10) for p in read_partition(os.path.join(storage, "sl", "fb", "0"))])
+    p1 = o.rescale(o.mul_relin_at(a, b, rlk, 12), 12)
+    p2 = o.mul_relin_at(p1, np.ascontiguousarray(b[:, :, :11]), rlk, 11)
+    qs = o.moduli[:11].astype(object)[None, None, :, None]
+    p3 = ((p2.astype(object) + c) % qs).astype(np.uint64)
+    assert np.array_equal(got, o.rescale(p3, 11))
 
 
 @pytest.mark.gpu
