@@ -10,6 +10,11 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -218,29 +223,96 @@ void PartitionWriter::commit() {
 // ------------------------------------------------------------- device state
 namespace {
 
-// f(i) for i in [0, n) on up to `threads` threads (contiguous chunks); the
-// first exception is rethrown after every thread has joined
+// A lane's IO helper threads, started once (per lane thread and size) and
+// parked on a condition variable between jobs: the per-batch row reads and
+// writes no longer spawn and join threads.  The calling thread takes chunk 0.
+class IoPool {
+ public:
+  explicit IoPool(unsigned threads) : threads_(threads) {
+    for (unsigned t = 1; t < threads_; ++t) workers_.emplace_back([this, t] { loop(t); });
+  }
+  ~IoPool() {
+    {
+      std::lock_guard lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &w : workers_) w.join();
+  }
+  IoPool(const IoPool &) = delete;
+  IoPool &operator=(const IoPool &) = delete;
+  unsigned size() const { return threads_; }
+
+  // f(i) for i in [0, n) in contiguous chunks; the first exception is rethrown
+  // after every chunk has finished
+  void run(size_t n, const std::function<void(size_t)> &f) {
+    {
+      std::lock_guard lk(m_);
+      job_ = &f;
+      n_ = n;
+      err_ = nullptr;
+      left_ = threads_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    chunk(0);
+    std::unique_lock lk(m_);
+    done_cv_.wait(lk, [this] { return left_ == 0; });
+    job_ = nullptr;
+    if (err_) std::rethrow_exception(err_);
+  }
+
+ private:
+  void chunk(unsigned t) {
+    try {
+      for (size_t i = n_ * t / threads_; i < n_ * (t + 1) / threads_; ++i) (*job_)(i);
+    } catch (...) {
+      std::lock_guard lk(m_);
+      if (!err_) err_ = std::current_exception();
+    }
+  }
+  void loop(unsigned t) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      chunk(t);
+      {
+        std::lock_guard lk(m_);
+        --left_;
+      }
+      done_cv_.notify_one();
+    }
+  }
+
+  const unsigned threads_;
+  std::vector<std::thread> workers_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)> *job_ = nullptr;
+  size_t n_ = 0;
+  unsigned left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  std::exception_ptr err_;
+};
+
+// f(i) for i in [0, n) on up to `threads` threads: the calling (lane) thread's
+// persistent IoPool of that size
 template <class F>
 void parallel_for(size_t n, unsigned threads, F f) {
-  threads = (unsigned)std::max<size_t>(1, std::min<size_t>(threads, n));
-  if (threads == 1) {
+  threads = std::max(1u, threads);
+  if (threads == 1 || n <= 1) {
     for (size_t i = 0; i < n; ++i) f(i);
     return;
   }
-  std::exception_ptr err;
-  std::mutex em;
-  std::vector<std::thread> pool;
-  for (unsigned t = 0; t < threads; ++t)
-    pool.emplace_back([&, t] {
-      try {
-        for (size_t i = n * t / threads; i < n * (t + 1) / threads; ++i) f(i);
-      } catch (...) {
-        std::lock_guard lk(em);
-        if (!err) err = std::current_exception();
-      }
-    });
-  for (auto &th : pool) th.join();
-  if (err) std::rethrow_exception(err);
+  thread_local std::unique_ptr<IoPool> pool;
+  if (!pool || pool->size() != threads) pool = std::make_unique<IoPool>(threads);
+  pool->run(n, std::function<void(size_t)>(f));
 }
 
 void ck(fhe_ctx *c, int rc, const char *what) {
@@ -895,25 +967,69 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
             break;
           }
         const size_t cw = s.ct_words(level);
+        const uint32_t op = mul ? FHE_REDUCE_MUL_RELIN : FHE_REDUCE_ADD;
+        const uint64_t *rlk = mul ? ks->relin.p : nullptr;
+        // Rows are staged max_batch at a time (two pinned slots, reused after
+        // their mark), so host and device memory stay bounded by the batch
+        // whatever the partitions hold.  Each chunk is reduced by the balanced
+        // tree of fhe_reduce_at; the chunk results merge like a binary counter
+        // (two partials of the same height combine, older one first), so at
+        // most log2(chunks) + 1 partials are alive.  A single chunk is the
+        // plain balanced tree.
+        const size_t C = std::max<uint32_t>(1, config_.max_batch);
+        struct Partial {
+          ArenaBuf buf;
+          uint32_t height;
+        };
+        std::vector<Partial> pend;
+        const auto combine = [&](const ArenaBuf &older, ArenaBuf &newer) {
+          if (mul) ck(s.ctx, fhe_mul_relin_at(s.ctx, older.p, newer.p, rlk, newer.p, 1, level), "reduce merge");
+          else ck(s.ctx, fhe_add_at(s.ctx, older.p, newer.p, newer.p, 1, level), "reduce merge");
+        };
+        ArenaBuf dev[2] = {ArenaBuf(*ls.arena, C * cw), ArenaBuf(*ls.arena, C * cw)};
+        bool used[2] = {false, false};
+        size_t pi = 0, ri = 0, k = 0;
+        while (pi < parts.size() && parts[pi]->size() == 0) ++pi;
+        while (pi < parts.size()) {
+          const int si = (int)(k++ & 1);
+          Slot &sl = ls.slot[si];
+          if (used[si]) ck(s.ctx, fhe_wait_mark(s.ctx, (uint32_t)si), "reduce slot wait");
+          if (sl.in.empty()) sl.in.push_back(std::make_unique<Pinned>());
+          uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[0]->reserve(s.ctx, C * cw * 8));
+          size_t m = 0;
+          for (; m < C && pi < parts.size(); ++m) {
+            CtHeader h;
+            parts[pi]->read(ri, 0, &h, sizeof(h));
+            if (check_ct_header(s, h) != level) throw std::runtime_error("reduce inputs differ in ciphertext level");
+            parts[pi]->read(ri, sizeof(h), host + m * cw, cw * 8);
+            if (++ri == parts[pi]->size()) {
+              ri = 0;
+              ++pi;
+              while (pi < parts.size() && parts[pi]->size() == 0) ++pi;
+            }
+          }
+          ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, dev[si].p, host, m * cw * 8), "h2d");
+          ck(s.ctx, fhe_mark(s.ctx, (uint32_t)si), "reduce slot mark");
+          used[si] = true;
+          Partial p{ArenaBuf(*ls.arena, cw), 0};
+          ck(s.ctx, fhe_reduce_at(s.ctx, dev[si].p, (uint32_t)m, op, rlk, p.buf.p, level), "reduce");
+          while (!pend.empty() && pend.back().height == p.height) {
+            combine(pend.back().buf, p.buf);
+            p.height += 1;
+            pend.pop_back();
+          }
+          pend.push_back(std::move(p));
+        }
+        while (pend.size() > 1) {  // fold the leftover partials, newest first
+          Partial p = std::move(pend.back());
+          pend.pop_back();
+          combine(pend.back().buf, p.buf);
+          pend.back().buf = std::move(p.buf);
+        }
         Slot &sl = ls.slot[0];
         sl.out_level = level;
-        if (sl.in.empty()) sl.in.push_back(std::make_unique<Pinned>());
-        uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[0]->reserve(s.ctx, count * cw * 8));
-        size_t r = 0;
-        for (const auto &pv : parts)
-          for (size_t i = 0; i < pv->size(); ++i, ++r) {
-            CtHeader h;
-            pv->read(i, 0, &h, sizeof(h));
-            if (check_ct_header(s, h) != level) throw std::runtime_error("reduce inputs differ in ciphertext level");
-            pv->read(i, sizeof(h), host + r * cw, cw * 8);
-          }
-        ArenaBuf a(*ls.arena, count * cw);
-        ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, a.p, host, count * cw * 8), "h2d");
-        // balanced tree, one batched add / mul+relin per level (fhe_reduce)
-        ck(s.ctx, fhe_reduce_at(s.ctx, a.p, (uint32_t)count, mul ? FHE_REDUCE_MUL_RELIN : FHE_REDUCE_ADD,
-                                mul ? ks->relin.p : nullptr, a.p, level), "reduce");
         uint64_t *res = reinterpret_cast<uint64_t *>(sl.out.reserve(s.ctx, cw * 8));
-        ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, res, a.p, cw * 8), "d2h");
+        ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, res, pend.back().buf.p, cw * 8), "d2h");
         ck(s.ctx, fhe_synchronize(s.ctx), "reduce sync");
         PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr),
                             config_.durable_outputs);

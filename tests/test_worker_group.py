@@ -233,6 +233,56 @@ def test_gpu_reduce_task_add_and_mul_trees(wg_run, tmp_path):
 
 
 @pytest.mark.gpu
+def test_gpu_reduce_task_chunked(wg_run, tmp_path):
+    """Rows staged max_batch (here 2) at a time: each chunk is a balanced tree,
+    the chunk results merge like a binary counter (older operand first).  CKKS
+    at level 7 (the rows' own level), 7 rows over 3 partitions, one empty."""
+    from oracle_ffi import SCHEME_CKKS
+    o, storage, keys = _setup(tmp_path, SCHEME_CKKS, 13, 8, 2, 3)
+    lvl = 7
+    parts = {"q0": 3, "q1": 0, "q2": 4}
+    cts, i = [], 0
+    for name, cnt in parts.items():
+        rows = []
+        for _ in range(cnt):
+            ct = o.uniform((1, 2, lvl, o.n), seed=200 + i)[0]
+            cts.append(ct)
+            rows.append(ct_row(o, [ct]))
+            i += 1
+        write_partition(os.path.join(storage, "s3", name, "0"), rows)
+    rlk = o.uniform(o.key_shape(), seed=29)
+    write_keys(os.path.join(keys, "s3", "0.key"), o, rlk, {})
+    env = dict(os.environ, WG_MAX_BATCH="2")
+    args = [wg_run, "reduce", storage, keys, "s3", "0", params_arg(o, str(tmp_path)), "outM", "0"]
+    r = subprocess.run(args + [f"{n}:0" for n in parts] + ["--", "mul"], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = parse_row(o, read_partition(os.path.join(storage, "s3", "outM", "0"))[0], level=lvl)
+
+    def mul(x, y):
+        return o.mul_relin_at(x[None], y[None], rlk, lvl)[0]
+
+    def tree(items):
+        live = list(items)
+        while len(live) > 1:
+            half = len(live) // 2
+            comb = [mul(live[j], live[len(live) - half + j]) for j in range(half)]
+            live = comb + live[half:len(live) - half]
+        return live[0]
+
+    pend = []
+    for c0 in range(0, len(cts), 2):
+        p, h = tree(cts[c0:c0 + 2]), 0
+        while pend and pend[-1][1] == h:
+            p, h = mul(pend.pop()[0], p), h + 1
+        pend.append((p, h))
+    while len(pend) > 1:
+        p = pend.pop()[0]
+        pend[-1] = (mul(pend[-1][0], p), pend[-1][1])
+    assert np.array_equal(got, pend[0][0])
+
+
+@pytest.mark.gpu
 def test_gpu_map_task_bfv(wg_run, tmp_path):
     from oracle_ffi import SCHEME_BFV
     o, storage, keys = _setup(tmp_path, SCHEME_BFV, 13, 3, 2, 2, t=65537)
