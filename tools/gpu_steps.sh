@@ -13,6 +13,8 @@
 #   stats          rocprofv3 --kernel-trace --stats of a short bench.py (roofline summary)
 #   steppmc        kernel trace + FETCH_SIZE + WRITE_SIZE passes of op_bench ckks_mul (128 per call):
 #                  summarise here with tools/step_summary.py -> profiles/<round>/step_summary.json
+#   optrace=OP     rocprofv3 --kernel-trace --stats of tools/op_bench.py OP (bfv_mul, ckks_mul, ckks_rot)
+#   prof           tools/profile_round.sh (roofline stats, PMC passes; summarise with tools/collect_profile.py)
 #   steptable      rocprofv3 kernel trace of one C5 wave loop -> tools/step_table.py
 set -e
 export TMPDIR=/tmp
@@ -47,6 +49,8 @@ for s in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/st_trace" -o run -- $B --reps 4 > "$O/st_trace.log" 2>&1
       timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/st_fetch" -o run -- $B --reps 2 > "$O/st_fetch.log" 2>&1
       timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/st_write" -o run -- $B --reps 2 > "$O/st_write.log" 2>&1 ;;
+    optrace=*) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/op_${s#optrace=}" -o run -- python3 tools/op_bench.py "${s#optrace=}" --batch 128 --reps 5 > "$O/op_${s#optrace=}.log" 2>&1 ;;
+    prof) timeout -k 10 1100 bash tools/profile_round.sh "$O/prof" > "$O/prof.log" 2>&1 ;;
     steptable) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/step" -o run -- python3 tools/op_bench.py ckks_mul --batch 128 --reps 8 > "$O/step.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
