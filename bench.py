@@ -564,6 +564,15 @@ def secondary_configs(hb, ctx, gk, a, b, out, dev, stream, B, reps):
     res["C4_ckks_rotate_per_s"] = round(B / t, 1)
     t = _timed(lambda: ctx.mul_relin(ct, b[:B], gk, o), reps, stream)
     res["C5_mul_relin_1ctx_per_s"] = round(B / t, 1)
+    # the CKKS multiply as a circuit runs it: mul+relin then rescale (12 -> 11 limbs),
+    # and the same product one level down (mul_relin_at on 11-limb ciphertexts)
+    r11 = hb.empty((B, 2, L - 1, 1 << LOG_N), device=dev)
+    t = _timed(lambda: (ctx.mul_relin(ct, b[:B], gk, o), ctx.rescale(o, r11, L)), reps, stream)
+    res["C5_mul_relin_rescale_1ctx_per_s"] = round(B / t, 1)
+    a11 = r11.clone()
+    t = _timed(lambda: ctx.mul_relin_at(a11, r11, gk, a11, L - 1), reps, stream)
+    res["C5_mul_relin_level11_1ctx_per_s"] = round(B / t, 1)
+    del r11, a11
     mods = openfhe_style_primes([(60, L), (61, K)], LOG_N)
     gen = hb.Context(hb.SCHEME_CKKS, LOG_N, L, K, DNUM, moduli=mods, device=dev.index)
     gen.set_stream(stream)
