@@ -39,20 +39,37 @@ def main(src, dst):
     tr = glob.glob(f"{src}/roofline/*kernel_trace.csv")
     if tr:
         per = {}
-        for r in csv.DictReader(open(tr[0])):
-            if "ntt_pass" in r["Kernel_Name"]:
-                per.setdefault(short(r["Kernel_Name"]), []).append(
+        rows = [r for r in csv.DictReader(open(tr[0])) if "ntt_pass" in r["Kernel_Name"]]
+        # only the roofline launches: the widest grid of each kernel (bench.py's
+        # per-rank self-check runs the same kernels over one ciphertext first)
+        gsz = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        widest = {}
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            widest[k] = max(widest.get(k, 0), gsz(r))
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            if gsz(r) == widest[k]:
+                per.setdefault(k, []).append(
                     (int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
         timed = {k: [d for _, d in sorted(v)[WARM:]] for k, v in per.items()}
         if all(timed.values()):
             ntt = {k: sum(v) / len(v) for k, v in timed.items()}
             launch_ns = sum(ntt.values())
+    # the roofline launches only: per counter file, the widest grid of each kernel
+    # (bench.py's per-rank self-check runs the same kernels over one ciphertext)
+    def roof_rows(f):
+        rs = [r for r in csv.DictReader(open(f)) if "ntt_pass" in r["Kernel_Name"]]
+        w = {}
+        for r in rs:
+            k = short(r["Kernel_Name"])
+            w[k] = max(w.get(k, 0), int(r["Grid_Size"]))
+        return [r for r in rs if int(r["Grid_Size"]) == w[short(r["Kernel_Name"])]]
+
     rows, fetch, write = [], {}, {}
     for tag, store in (("pmc_fetch", fetch), ("pmc_write", write)):
         for f in glob.glob(f"{src}/{tag}/*counter_collection.csv"):
-            for r in csv.DictReader(open(f)):
-                if "ntt_pass" not in r["Kernel_Name"]:
-                    continue
+            for r in roof_rows(f):
                 k = short(r["Kernel_Name"])
                 store.setdefault(k, []).append(float(r["Counter_Value"]))
                 rows.append({"kernel": k, "counter": r["Counter_Name"], "value": r["Counter_Value"],
@@ -62,9 +79,7 @@ def main(src, dst):
     # 8 XCDs' busy cycles; 1024 SIMDs.
     valu = {}
     for f in glob.glob(f"{src}/pmc_valu/*counter_collection.csv"):
-        for r in csv.DictReader(open(f)):
-            if "ntt_pass" not in r["Kernel_Name"]:
-                continue
+        for r in roof_rows(f):
             k = short(r["Kernel_Name"])
             valu.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
             rows.append({"kernel": k, "counter": r["Counter_Name"], "value": r["Counter_Value"],
@@ -73,9 +88,7 @@ def main(src, dst):
     mix = {}
     for tag in ("pmc_valu", "pmc_mix"):
         for f in glob.glob(f"{src}/{tag}/*counter_collection.csv"):
-            for r in csv.DictReader(open(f)):
-                if "ntt_pass" not in r["Kernel_Name"]:
-                    continue
+            for r in roof_rows(f):
                 mix.setdefault(short(r["Kernel_Name"]), {}).setdefault(r["Counter_Name"], []).append(
                     float(r["Counter_Value"]))
     valu_busy = {}
