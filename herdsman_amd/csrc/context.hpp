@@ -105,6 +105,7 @@ struct fhe_ctx {
   u32 key_qp = 0;                // key rows per digit half (0: L + K)
   u32 key_pshift = 0;            // L_parent - m for a view
   u64 *d_qdrop = nullptr;        // view at level m: [2m] = q_m^-1 R mod q_i, then q_m mod q_i (rescale m+1 -> m)
+  ConvTab lift{};                // view at level m: the 1-source "conversion" of the rescale lift, h = R mod q_i
 };
 
 // key layout of a context (level views read the parent's full-level keys)
@@ -173,9 +174,18 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale = false,
 // ext / ksk: acc's Q limbs are the key-switching inner product of ext [n][ndig][QP][N]
 // with ksk [ndig][2][QP][N], formed in the last pass instead of read (EPI_KSQ)
 // pinv: the epilogue's per-limb constant (null: P^-1, d_pinv; rescale: q_last^-1, d_qdrop)
+// pro_src: the prologue's sources (null: acc's P limbs, ModDown); rescale passes
+// the dropped limb with its central-lift constants
+struct ConvSrc {
+  const u64 *src;      // [n_polys][stride][N]
+  u32 stride, first;
+  u64 lift_half;       // 0: plain conversion
+  const u64 *lift_sub;  // [nd] device
+};
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro = nullptr, const u64 *ext = nullptr,
-                           const u64 *ksk = nullptr, u32 ndig = 0, u32 base_g = 0, const u64 *pinv = nullptr);
+                           const u64 *ksk = nullptr, u32 ndig = 0, u32 base_g = 0, const u64 *pinv = nullptr,
+                           const ConvSrc *pro_src = nullptr);
 // ModUp of digit j fused into the column pass of the forward NTT of its
 // converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive

@@ -200,6 +200,9 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p, u32 alpha = 0) {
   c->nB = p->scheme == FHE_SCHEME_BFV ? c->L + 1 : 0;
   c->nmod = c->L + c->K + c->nB;
   if (p->scheme > FHE_SCHEME_BFV) return fhe_fail(c, FHE_ERR_INVALID, "unknown scheme");
+  if (p->flags & ~FHE_FLAG_BFV_HPS) return fhe_fail(c, FHE_ERR_INVALID, "unknown fhe_params.flags bits");
+  if ((p->flags & FHE_FLAG_BFV_HPS) && p->scheme != FHE_SCHEME_BFV)
+    return fhe_fail(c, FHE_ERR_INVALID, "FHE_FLAG_BFV_HPS on a CKKS context");
   if (p->log_n < 10 || p->log_n > 17) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "log_n must be in [10, 17]");
   if (c->L == 0 || c->dnum == 0 || c->dnum > c->L) return fhe_fail(c, FHE_ERR_INVALID, "need 1 <= dnum <= L");
   if (c->alpha > 16) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "alpha = ceil(L/dnum) must be <= 16");
@@ -355,7 +358,13 @@ int ctx_level(fhe_ctx *c, u32 m, fhe_ctx **out) {
         qd[m + i] = qm % qi;
       }
       v->d_qdrop = (u64 *)ctx_upload(v, qd.data(), sizeof(u64) * qd.size());
-      if (!v->d_qdrop) rc = fhe_fail(v, FHE_ERR_OOM, "level view tables");
+      // the rescale lift as a 1-source conversion prologue: h = R mod q_i (y = x mod q_i)
+      std::vector<u64> h1(m);
+      for (u32 i = 0; i < m; ++i) h1[i] = tomont(1, r->moduli[i]);
+      v->lift.ns = 1;
+      v->lift.nd = m;
+      v->lift.h = (const u64 *)ctx_upload(v, h1.data(), sizeof(u64) * m);
+      if (!v->d_qdrop || !v->lift.h) rc = fhe_fail(v, FHE_ERR_OOM, "level view tables");
     }
     if (rc) {
       fhe_fail(c, rc, "level view: " + v->err);

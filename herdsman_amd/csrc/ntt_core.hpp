@@ -126,6 +126,10 @@ struct NttArgs {
   const u64 *c_src;
   const u64 *c_h;        // [ns][nd] ConvTab.h
   u32 c_src_stride, c_src_first, c_ns, c_nd;
+  // one source only (rescale): the central lift of the dropped limb, y - [q_l]_{q_m}
+  // where the source word exceeds c_lift_half (0: plain conversion)
+  u64 c_lift_half;
+  const u64 *c_lift_sub;  // [nd] q_l mod q_m
 };
 
 // The passes shared by several entry points, compiled once (ntt.hip, ntt_conv*.hip):
@@ -189,6 +193,7 @@ struct EpiRow {
   u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is
   const u64 *src;  // PRO_CONV: source limb 0 of this poly (limb i at src + i N)
   u64 h[4];        // PRO_CONV: h[i][m] of this workgroup's target limb
+  u64 lift_sub;    // PRO_CONV, one source, rescale lift: q_l mod q_m
 };
 
 // LDS slot of element k of sub-transform w: one pad word per 16 words and per
@@ -740,6 +745,15 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
           x[c0 + j] = CONV_COLS && SP && WIDE && CONV_SP60 ? dot_cols_sp60<NS>(sv[j], hc0, hc1, mi.q_hi)  // < 2q
                       : CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                                  // < 2q
                                   : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);                   // < 4q
+        if constexpr (NS == 1 && CONV_COLS) {
+          // rescale: the central lift (x - q_l for x > q_l / 2) of the single
+          // source, as y + q - [q_l]_{q_m} < 3q (a uniform branch per launch)
+          if (a.c_lift_half) {
+            const u64 add = mi.q - ep.lift_sub;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[c0 + j] += sv[j][0] > a.c_lift_half ? add : 0;
+          }
+        }
       }
     } else {
       // the first forward pass may read out of place (NttArgs::src)
@@ -919,6 +933,7 @@ __global__ void __launch_bounds__(W << (S - LOGR),
     ep.src = a.c_src + (((size_t)poly * a.c_src_stride + a.c_src_first) << LOG_N);
 #pragma unroll
     for (int i = 0; i < conv_ns(EPI); ++i) ep.h[i] = a.c_h[(size_t)i * a.c_nd + act];
+    if (conv_ns(EPI) == 1 && a.c_lift_sub) ep.lift_sub = a.c_lift_sub[act];
   }
   if constexpr (!INV && WM == 2) {
     // WIDE lazy schedule for moduli below 2^60 (per-workgroup uniform branch)

@@ -11,7 +11,7 @@
 // forms acc[2 ct + b][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1 itself.
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro, const u64 *ext, const u64 *ksk, u32 ndig,
-                           u32 base_g, const u64 *pinv) {
+                           u32 base_g, const u64 *pinv, const ConvSrc *pro_src) {
   const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
   if (ext && (c->log_n <= 14 || ndig > 4 || (n_polys & 1)))
@@ -48,9 +48,17 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
       if (pro) {
         // the ModDown conversion P -> Q as the column pass's prologue: the
         // sources are acc's P limbs, already scaled by the INTT (d_iscale)
-        a.c_src = acc + (size_t)p0 * acc_stride * N;
-        a.c_src_stride = acc_stride;
-        a.c_src_first = L;
+        if (pro_src) {
+          a.c_src = pro_src->src + (size_t)p0 * pro_src->stride * N;
+          a.c_src_stride = pro_src->stride;
+          a.c_src_first = pro_src->first;
+          a.c_lift_half = pro_src->lift_half;
+          a.c_lift_sub = pro_src->lift_sub;
+        } else {
+          a.c_src = acc + (size_t)p0 * acc_stride * N;
+          a.c_src_stride = acc_stride;
+          a.c_src_first = L;
+        }
         a.c_ns = pro->ns;
         a.c_nd = pro->nd;
         a.c_h = pro->h;

@@ -950,6 +950,14 @@ int rescale_impl(fhe_ctx *up, fhe_ctx *lo, const u64 *ct, u64 *out, u32 n) {
     return rc;
   if ((rc = ntt_launch(up, LimbMap{x, 1, 1, 0, 1, 0, m, 2 * n}, true))) return rc;
   const u64 qm = up->moduli[m];
+  if (lo->log_n >= 15) {
+    // two-pass sizes: the lift runs as the 1-source conversion prologue of the
+    // NTT's column pass (PRO_CONV with the central-lift step), so the lifted
+    // limbs never make an HBM round trip
+    const ConvSrc src{x, 1, 0, qm >> 1, lo->d_qdrop + m};
+    return ntt_fwd_combine_launch(lo, conv, 2 * n, ct, m + 1, out, out, 0u, &lo->lift, nullptr, nullptr, 0, 0,
+                                  lo->d_qdrop, &src);
+  }
   if ((rc = SP_DISPATCH(lo, rescale_lift, lo, x, conv, lo->d_qdrop + m, qm >> 1, 2 * n))) return rc;
   return ntt_fwd_combine_launch(lo, conv, 2 * n, ct, m + 1, out, out, 0u, nullptr, nullptr, nullptr, 0, 0,
                                 lo->d_qdrop);

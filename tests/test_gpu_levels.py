@@ -211,3 +211,19 @@ def test_level_reduce_and_reduce_at(hb, metric):
         comb = o.mul_relin_at(np.stack(live[:half]), np.stack(live[len(live) - half:]), k, lvl)
         live = list(comb) + live[half:len(live) - half]
     assert np.array_equal(hb.to_host(res)[0], live[0])
+
+
+@pytest.mark.parametrize("log_n", [15, 14])
+def test_rescale_generic_primes(hb, log_n):
+    """OpenFHE-style primes (q = 1 mod 2N, generic Montgomery; 55- and 61-bit so
+    the fused lift meets both lazy schedules) at a two-pass size (the lift in the
+    column pass prologue) and a one-pass size (the lift kernel)."""
+    from herdsman_amd.params import openfhe_style_primes
+    mods = openfhe_style_primes([(55, 3), (61, 3), (61, 2)], log_n)
+    o = Oracle(SCHEME_CKKS, log_n, 6, 2, 3, moduli=mods)
+    c = hb.Context(SCHEME_CKKS, log_n, 6, 2, 3, moduli=o.moduli)
+    for lvl in (6, 4):
+        ct = o.uniform((2, 2, lvl, o.n), seed=900 + lvl)
+        out = hb.empty((2, 2, lvl - 1, o.n))
+        c.rescale(hb.to_device(ct), out, lvl)
+        assert np.array_equal(hb.to_host(out), o.rescale(ct, lvl)), lvl

@@ -387,6 +387,10 @@ def test_errors_are_loud(hb):
         c.mul_relin(hb.empty((1, 2, 2, 1 << 12)), hb.empty((1, 2, 2, 1 << 12)), x, hb.empty((1, 2, 2, 1 << 12)))
     with pytest.raises(hb.FheBackendError):
         hb.Context(SCHEME_CKKS, 9, 2)  # N below the supported range
+    with pytest.raises(hb.FheBackendError, match="CKKS context"):
+        hb.Context(SCHEME_CKKS, 12, 2, 1, 1, bfv_mult="hps")  # HPS is a BFV technique
+    with pytest.raises(hb.FheBackendError, match="unknown BFV"):
+        hb.Context(SCHEME_BFV, 12, 2, 1, 1, t=65537, bfv_mult="behz+")
 
 
 # ------------------------------------------------------------ edge values
