@@ -89,6 +89,7 @@ SIGNATURES = {
     "fhe_reduce": (C.c_int, [_vp, _vp, _u32, C.c_int, _vp, _vp]),
     "fhe_bcast_key": (C.c_int, [_vp, _vp, _sz, _vp, C.c_int]),
     "fhe_reduce_ranks": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, C.c_int, _vp]),
+    "fhe_reduce_ranks_at": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp, C.c_int, _vp, _u32]),
     "fhe_reduce_schedule": (C.c_int, [C.c_int, C.c_int, C.c_int, _vp, C.c_int]),
 }
 

@@ -809,6 +809,14 @@ int fhe_reduce_schedule(int rank, int world, int root, int32_t *steps, int cap) 
   return n;
 }
 
+int fhe_reduce_ranks_at(fhe_ctx *c, uint64_t *ct, int op, const uint64_t *rlk, void *comm, int root, uint64_t *tmp,
+                        uint32_t level) {
+  fhe_ctx *v;
+  DeviceBind bind(c);
+  int rc = at_level(c, level, &v);
+  return rc ? rc : from_view(c, v, fhe_reduce_ranks(v, ct, op, rlk, comm, root, tmp));
+}
+
 int fhe_reduce_ranks(fhe_ctx *c, uint64_t *ct, int op, const uint64_t *rlk, void *comm, int root, uint64_t *tmp) {
   if (!c) return FHE_ERR_INVALID;
   DeviceBind bind(c);

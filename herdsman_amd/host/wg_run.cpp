@@ -15,7 +15,7 @@
 //                 (partition read, PCIe both ways, GPU, partition write): the
 //                 mean and spread of REPS (default 5) warm repetitions after one
 //                 warm-up, and where the lanes' time went (GpuWorkerGroup::stage_stats).
-// PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file]   PROGRAM tokens: in<i> add sub mul rot:<k> rescale
+// PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file[,behz|hps]]   PROGRAM tokens: in<i> add sub mul rot:<k> rescale
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -52,7 +52,7 @@ static herdsman_gpu::SchemaParams parse_params(int schema, const std::string &sp
   std::string tok;
   std::vector<std::string> v;
   while (std::getline(ss, tok, ',')) v.push_back(tok);
-  if (v.size() < 6) throw std::runtime_error("PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file]");
+  if (v.size() < 6) throw std::runtime_error("PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file[,behz|hps]]");
   sp.params.scheme = std::stoul(v[0]);
   sp.params.log_n = std::stoul(v[1]);
   sp.params.num_q = std::stoul(v[2]);
@@ -61,10 +61,14 @@ static herdsman_gpu::SchemaParams parse_params(int schema, const std::string &sp
   sp.params.plain_modulus = std::stoull(v[5]);
   sp.params.q_bits = 60;
   sp.params.p_bits = 61;
-  if (v.size() > 6) {
+  if (v.size() > 6 && !v[6].empty()) {
     std::ifstream in(v[6]);
     uint64_t q;
     while (in >> q) sp.moduli.push_back(q);
+  }
+  if (v.size() > 7) {  // BFV multiplication technique
+    if (v[7] == "hps") sp.params.flags |= FHE_FLAG_BFV_HPS;
+    else if (v[7] != "behz") throw std::runtime_error("PARAMS mult must be behz or hps");
   }
   return sp;
 }

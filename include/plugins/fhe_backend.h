@@ -201,6 +201,9 @@ int fhe_bcast_key(fhe_ctx *ctx, uint64_t *key, size_t words, void *nccl_comm, in
  * The result is in `ct` on root; tmp is one ciphertext of device scratch. */
 int fhe_reduce_ranks(fhe_ctx *ctx, uint64_t *ct, int op, const uint64_t *rlk, void *nccl_comm, int root,
                      uint64_t *tmp);
+/* the same on ciphertexts of level `level` (ct, tmp: [2][level][N]; CKKS) */
+int fhe_reduce_ranks_at(fhe_ctx *ctx, uint64_t *ct, int op, const uint64_t *rlk, void *nccl_comm, int root,
+                        uint64_t *tmp, uint32_t level);
 /* The tree of fhe_reduce_ranks, host only: writes the rank's steps in order,
  * peer + 1 for "receive from peer and combine", -(peer + 1) for "send to peer
  * (then stop)"; returns the number of steps (<= cap) or a negative error. */

@@ -555,6 +555,13 @@ def test_rccl_entry_points_single_rank(hb):
         assert np.array_equal(hb.to_host(dk), key)
         assert np.array_equal(hb.to_host(dct), ct)
         assert lib.fhe_reduce_ranks(c.h, dct.data_ptr(), 7, None, comm, 0, tmp.data_ptr()) == hb.FHE_ERR_INVALID
+        # the same join on a level-2 ciphertext (a level view of the context)
+        ct2 = np.ascontiguousarray(ct[:, :, :2])
+        d2, t2 = hb.to_device(ct2), hb.empty(ct2.shape)
+        rc = lib.fhe_reduce_ranks_at(c.h, d2.data_ptr(), hb.REDUCE_ADD, None, comm, 0, t2.data_ptr(), 2)
+        assert rc == 0, lib.fhe_last_error(c.h)
+        torch.cuda.synchronize()
+        assert np.array_equal(hb.to_host(d2), ct2)
     finally:
         rccl.ncclCommDestroy(comm)
 

@@ -283,9 +283,12 @@ def test_gpu_reduce_task_chunked(wg_run, tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_map_task_bfv(wg_run, tmp_path):
-    from oracle_ffi import SCHEME_BFV
+@pytest.mark.parametrize("mult", ["behz", "hps"])
+def test_gpu_map_task_bfv(wg_run, tmp_path, mult):
+    from oracle_ffi import Oracle, SCHEME_BFV
     o, storage, keys = _setup(tmp_path, SCHEME_BFV, 13, 3, 2, 2, t=65537)
+    if mult == "hps":
+        o = Oracle(SCHEME_BFV, 13, 3, 2, 2, t=65537, bfv_mult="hps")
     rows = 3
     a = o.uniform((rows, 2, o.L, o.n), seed=21)
     b = o.uniform((rows, 2, o.L, o.n), seed=22)
@@ -293,8 +296,8 @@ def test_gpu_map_task_bfv(wg_run, tmp_path):
     write_partition(os.path.join(storage, "sb", "in", "0"), [ct_row(o, [a[i], b[i]]) for i in range(rows)])
     write_keys(os.path.join(keys, "sb", "1.key"), o, rlk, {})
     # (in0 * in1) + in0
-    r = subprocess.run([wg_run, "map", storage, keys, "sb", "1", params_arg(o, str(tmp_path)), "in", "0", "out",
-                        "in0", "in1", "mul", "in0", "add"], capture_output=True, text=True, timeout=600)
+    r = subprocess.run([wg_run, "map", storage, keys, "sb", "1", params_arg(o, str(tmp_path)) + "," + mult, "in",
+                        "0", "out", "in0", "in1", "mul", "in0", "add"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     got = np.stack([parse_row(o, p) for p in read_partition(os.path.join(storage, "sb", "out", "0"))])
     assert np.array_equal(got, o.ct_add(o.mul_relin(a, b, rlk), a))
