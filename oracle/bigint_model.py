@@ -215,7 +215,7 @@ class Params:
 
 
 # ------------------------------------------------------- hybrid keyswitch
-def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = None):
+def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = None, ext_g: int = 0):
     """Hybrid key switching at level lvl (default L).  d: lvl limbs (NTT form if
     ntt_form).  ksk[j][b][i] limb i of Q u P of the FULL-level key (NTT form);
     at a reduced level the digits partition the lvl active limbs by alpha and
@@ -240,6 +240,8 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = Non
             ext[i] = dn[i]
         for i, c in zip(others, conv_n):
             ext[i] = c
+        if ext_g:  # hoisted rotation: sigma_g applied to the digit's extension
+            ext = {i: automorph_ntt(e, ext_g) for i, e in ext.items()}
         for b in range(2):
             for i in QP:
                 q = p.moduli[mi[i]]
@@ -331,6 +333,17 @@ def rotate(p: Params, ct, g: int, gk):
         c1 = [automorph_coef(x, g, p.moduli[i]) for i, x in enumerate(ct[1])]
     ks0, ks1 = keyswitch(p, c1, gk, p.scheme == "ckks")
     return [[[(x + y) % p.moduli[i] for x, y in zip(c0[i], ks0[i])] for i in range(L)], ks1]
+
+
+def rotate_hoisted(p: Params, ct, gs, gks):
+    """CKKS rotations of one ciphertext by every g in gs sharing one ModUp of
+    c1: KS over sigma_g(ModUp(c1)) with key gks[r] (OpenFHE EvalFastRotation)."""
+    out = []
+    for g, gk in zip(gs, gks):
+        c0 = [automorph_ntt(x, g) for x in ct[0]]
+        ks0, ks1 = keyswitch(p, ct[1], gk, True, None, g)
+        out.append([[[(x + y) % p.moduli[i] for x, y in zip(c0[i], ks0[i])] for i in range(p.L)], ks1])
+    return out
 
 
 # -------------------------------------------------------------- BFV BEHZ

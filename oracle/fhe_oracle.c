@@ -400,8 +400,19 @@ void orc_base_conv(const orc_ctx *c, const uint64_t *src, const uint32_t *src_mo
  * sum_j [d]_{Q_j} g_j = P d mod q_i; OpenFHE's KeySwitchHYBRID at a reduced
  * level).  Level space: index i < lvl is q_i, lvl + k is p_k (modulus L + k).
  * in_ntt: 1 if d (and the result) is in NTT form (CKKS), 0 for coef form (BFV). */
+/* ext_g != 0 (hoisted rotation, CKKS): the digits' extensions are computed for d
+ * and then permuted by the NTT-domain automorphism sigma_g before the inner
+ * product, i.e. sigma_g(ModUp(d)) stands in for ModUp(sigma_g(d)) -- the same
+ * key-switching input up to its ModUp error term, so the bits differ from the
+ * plain rotation's (OpenFHE EvalFastRotation on precomputed digits). */
+static void keyswitch_lvl_g(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, int in_ntt,
+                            uint32_t lvl, uint32_t ext_g);
 static void keyswitch_lvl(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, int in_ntt,
                           uint32_t lvl) {
+  keyswitch_lvl_g(c, d, ksk, out, in_ntt, lvl, 0);
+}
+static void keyswitch_lvl_g(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, int in_ntt,
+                            uint32_t lvl, uint32_t ext_g) {
   const uint32_t n = c->n, L = lvl, K = c->K, QP = L + K, QPk = c->L + K, A = c->alpha;
 #define MI(i) ((i) < L ? (i) : c->L + ((i) - L))
   uint64_t *dc = malloc(sizeof(uint64_t) * L * n);        /* d in coef form */
@@ -426,6 +437,12 @@ static void keyswitch_lvl(const orc_ctx *c, const uint64_t *d, const uint64_t *k
     conv_tab_init(T, sq, hi - lo, dq, nd);
     conv_apply(T, sp, dp, n);
     for (uint32_t k = 0; k < nd; ++k) ntt_fwd_limb(&c->m[MI(didx[k])], ext + (size_t)didx[k] * n, n);
+    if (ext_g) {  /* hoisted rotation: sigma_g on the digit's extension (a slot permutation per limb) */
+      uint64_t *tmp = malloc(sizeof(uint64_t) * QP * n);
+      orc_automorph_ntt(c, ext, tmp, ext_g, 1, QP);
+      memcpy(ext, tmp, sizeof(uint64_t) * QP * n);
+      free(tmp);
+    }
     /* inner product with key digit j (its rows of Q_lvl u P) */
     for (uint32_t b = 0; b < 2; ++b) {
       const uint64_t *kj = ksk + ((size_t)(j * 2 + b) * QPk) * n;
@@ -839,6 +856,27 @@ static void rotate_lvl(const orc_ctx *c, const uint64_t *ct, uint32_t g, const u
 void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
                 uint32_t n_ct) {
   rotate_lvl(c, ct, g, gk, out, n_ct, c->L);
+}
+
+/* Hoisted rotations (CKKS): for each Galois element g_r of galois[0..n_rot),
+ * outs[r] = (sigma(c0) + KS0, KS1) with KS over sigma_g(ModUp(c1)) and key
+ * gks[r] -- one ModUp of c1 serves every rotation.  gks [n_rot][key],
+ * outs [n_rot][n_ct][2][L][N]. */
+void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                        const uint64_t *gks, uint64_t *outs, uint32_t n_ct) {
+  const size_t L = c->L, N = c->n, CT = 2 * L * N, KW = (size_t)c->dnum * 2 * (c->L + c->K) * N;
+  for (uint32_t r = 0; r < n_rot; ++r) {
+#pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
+    for (long i = 0; i < (long)n_ct; ++i) {
+      uint64_t *o = outs + ((size_t)r * n_ct + i) * CT;
+      uint64_t *ks = malloc(sizeof(uint64_t) * CT);
+      keyswitch_lvl_g(c, ct + i * CT + L * N, gks + r * KW, ks, 1, (uint32_t)L, galois[r]);
+      orc_automorph_ntt(c, ct + i * CT, o, galois[r], 1, (uint32_t)L);
+      orc_add(c, o, ks, o, 1, 0, (uint32_t)L);
+      memcpy(o + L * N, ks + L * N, sizeof(uint64_t) * L * N);
+      free(ks);
+    }
+  }
 }
 
 /* ------------------------------------------------- CKKS levels (rescale) */

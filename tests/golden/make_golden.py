@@ -120,6 +120,23 @@ def gen_bfv_hps(rng):
              out_mul=arr(out_mul))
 
 
+def gen_ckks_hoisted(rng):
+    """Hoisted CKKS rotations (one ModUp of c1, sigma_g on the extensions) for
+    steps 1, -3 and conjugation, each with its own key."""
+    log_n, L, K, dnum = 10, 5, 2, 2
+    n = 1 << log_n
+    Q = M.gen_primes(60, log_n, L)
+    P = M.gen_primes(61, log_n, K, exclude=Q)
+    p = M.Params(log_n, L, K, dnum, Q + P, "ckks")
+    ct = [rand_limbs(rng, Q, n) for _ in range(2)]
+    gs = [M.galois_elt(log_n, 1), M.galois_elt(log_n, -3), 2 * n - 1]
+    gks = [[[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(dnum)] for _ in gs]
+    out = M.rotate_hoisted(p, ct, gs, gks)
+    np.savez(os.path.join(HERE, "ckks_hoisted_n1024_l5.npz"), log_n=np.uint32(log_n), L=np.uint32(L),
+             K=np.uint32(K), dnum=np.uint32(dnum), moduli=arr(Q + P), ct=arr(ct),
+             galois=np.array(gs, dtype=np.uint32), gks=arr(gks), out=arr(out))
+
+
 def gen_ckks_levels(rng):
     """CKKS at reduced levels: L = 5 primes, alpha = 3 (dnum 2), so level 4 has
     a partial second digit, level 3 one full digit and level 2 one partial
@@ -159,6 +176,7 @@ def main():
     gen_bfv(rng)
     gen_ckks_levels(random.Random(0x4C564C53))
     gen_bfv_hps(random.Random(0x485053))
+    gen_ckks_hoisted(random.Random(0x484F4953))
     print("golden vectors written to", HERE)
 
 
@@ -167,5 +185,7 @@ if __name__ == "__main__":
         gen_ckks_levels(random.Random(0x4C564C53))
     elif sys.argv[1:] == ["hps"]:
         gen_bfv_hps(random.Random(0x485053))
+    elif sys.argv[1:] == ["hoisted"]:
+        gen_ckks_hoisted(random.Random(0x484F4953))
     else:
         main()

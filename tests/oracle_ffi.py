@@ -64,6 +64,7 @@ def lib():
         "orc_mul_relin_at": (None, [vp, _u64p, _u64p, _u64p, _u64p, u32, u32]),
         "orc_rotate_at": (None, [vp, _u64p, u32, _u64p, _u64p, u32, u32]),
         "orc_rescale": (None, [vp, _u64p, _u64p, u32, u32]),
+        "orc_rotate_hoisted": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32]),
         "orc_fill_uniform": (None, [vp, _u64p, u32, u32, u32, u64]),
         "orc_sample_ternary": (None, [vp, u64, _i64p]),
         "orc_sample_cbd": (None, [vp, u64, _i64p]),
@@ -162,6 +163,14 @@ class Oracle:
     def keyswitch_at(self, d, ksk, lvl):
         out = np.zeros((d.shape[0], 2, lvl, self.n), dtype=np.uint64)
         self.lib.orc_keyswitch_at(self.h, np.ascontiguousarray(d), np.ascontiguousarray(ksk), out, d.shape[0], lvl)
+        return out
+
+    def rotate_hoisted(self, ct, galois, gks):
+        """ct [n][2][L][N], galois [r], gks [r][key] -> [r][n][2][L][N]"""
+        ct = np.ascontiguousarray(ct)
+        gs = np.ascontiguousarray(galois, dtype=np.uint32)
+        out = np.zeros((len(gs),) + ct.shape, dtype=np.uint64)
+        self.lib.orc_rotate_hoisted(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), out, ct.shape[0])
         return out
 
     def rescale(self, ct, lvl):

@@ -129,3 +129,10 @@ def test_bfv_hps_mul_relin_golden():
                moduli=g["moduli"], bfv_mult="hps")
     out = o.mul_relin(g["a"][None], g["b"][None], g["rlk"])
     assert np.array_equal(out[0], g["out_mul"])
+
+
+def test_ckks_hoisted_rotations_golden():
+    g = load("ckks_hoisted_n1024_l5.npz")
+    o = Oracle(SCHEME_CKKS, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), moduli=g["moduli"])
+    out = o.rotate_hoisted(g["ct"][None], g["galois"], g["gks"])
+    assert np.array_equal(out[:, 0], g["out"])

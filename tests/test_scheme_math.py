@@ -95,3 +95,23 @@ def test_bfv_mul_relin_decrypts_exactly(mult):
     gk = o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=8)
     rot = o.rotate(c1[None], g, gk)[0]
     assert dec(rot) == [v % t for v in automorph_int(m1, g)]
+
+
+def test_ckks_hoisted_rotations_decrypt():
+    """Hoisted rotations (one ModUp shared) decrypt to the rotated message with
+    real Galois keys, like the plain rotation."""
+    o = Oracle(SCHEME_CKKS, 10, 4, 2, 2)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    s, s_qp = _keys(o)
+    rng = random.Random(7)
+    delta = 1 << 40
+    u = [rng.randint(-100, 100) for _ in range(o.n)]
+    ct = o.encrypt(to_rns([delta * x for x in u], Q), s_qp, 707)
+    steps = (1, 5, -3)
+    gs = [o.galois_elt(k) for k in steps]
+    gks = np.stack([o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=30 + i) for i, g in enumerate(gs)])
+    outs = o.rotate_hoisted(ct[None], gs, gks)
+    for r, g in enumerate(gs):
+        dec = crt_centered(o.decrypt(outs[r, 0], s_qp), Q)
+        want = [delta * v for v in automorph_int(u, g)]
+        assert max(abs(a - b) for a, b in zip(dec, want)) < 2 ** 30
