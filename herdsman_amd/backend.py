@@ -78,6 +78,8 @@ SIGNATURES = {
     "fhe_keyswitch": (C.c_int, [_vp, _vp, _vp, _vp, _u32]),
     "fhe_rotate": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _u32]),
     "fhe_galois_elt": (C.c_int, [_vp, _i32, C.POINTER(_u32)]),
+    "fhe_rotate_hoisted": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32]),
+    "fhe_rotate_hoisted_at": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32]),
     "fhe_add_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
     "fhe_sub_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
     "fhe_mul_relin_at": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _u32, _u32]),
@@ -301,6 +303,24 @@ class Context:
         self._ck(self.lib.fhe_rotate(self.h, _ptr(ct), galois, _ptr(gk), _ptr(out), n), "fhe_rotate")
         return out
 
+    def _hoisted(self, fn, ct, galois, gks, outs, n, *extra):
+        if not (len(galois) == len(gks) == len(outs)):
+            raise FheBackendError("hoisted rotations: galois, gks and outs must have one length")
+        for k in gks:
+            self._key(k)
+        nr = len(galois)
+        ga = np.ascontiguousarray(galois, dtype=np.uint32)
+        ka = (C.c_uint64 * max(nr, 1))(*[_ptr(k) for k in gks])
+        oa = (C.c_uint64 * max(nr, 1))(*[_ptr(o) for o in outs])
+        self._ck(fn(self.h, _ptr(ct), nr, ga.ctypes.data, C.addressof(ka), C.addressof(oa), n, *extra),
+                 fn.__name__)
+        return outs
+
+    def rotate_hoisted(self, ct, galois, gks, outs):
+        """CKKS: outs[r] = rotation of ct by galois[r] with key gks[r], one ModUp of c1 for all."""
+        n = self._ct_batch(ct, *outs)
+        return self._hoisted(self.lib.fhe_rotate_hoisted, ct, galois, gks, outs, n)
+
     # ---- CKKS levels: ciphertexts [n][2][level][N] over the first `level` Q primes
     def _ct_level(self, level: int, *cts):
         if not 1 <= level <= self.L:
@@ -335,6 +355,10 @@ class Context:
         self._key(gk)
         self._ck(self.lib.fhe_rotate_at(self.h, _ptr(ct), galois, _ptr(gk), _ptr(out), n, level), "fhe_rotate_at")
         return out
+
+    def rotate_hoisted_at(self, ct, galois, gks, outs, level: int):
+        n = self._ct_level(level, ct, *outs)
+        return self._hoisted(self.lib.fhe_rotate_hoisted_at, ct, galois, gks, outs, n, level)
 
     def keyswitch_at(self, d, ksk, out, level: int):
         n = self._ct_level(level, out)

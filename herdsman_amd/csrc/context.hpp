@@ -185,7 +185,7 @@ struct ConvSrc {
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro = nullptr, const u64 *ext = nullptr,
                            const u64 *ksk = nullptr, u32 ndig = 0, u32 base_g = 0, const u64 *pinv = nullptr,
-                           const ConvSrc *pro_src = nullptr);
+                           const ConvSrc *pro_src = nullptr, u32 ext_g = 0);
 // ModUp of digit j fused into the column pass of the forward NTT of its
 // converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
@@ -193,7 +193,8 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
 int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j);
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n);
 // INTT(acc_P) with the P limbs' key-switching inner product in its first pass
-int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig);
+// (ext_g != 0: ext is read as sigma_g(ext), the hoisted rotation's inner product)
+int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, u32 ext_g = 0);
 // (base null: sigma(c0) is not stored; the combine then reads it with base_g)
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);
@@ -207,6 +208,11 @@ int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u
                  u32 add_mask, bool ntt_form, u64 *ws);
 int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n);
 int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n, bool ntt_form);
+// CKKS hoisted rotations: one ModUp of c1 serves n_rot Galois elements
+// (outs[r] [n][2][L][N], apart from ct; gks[r] device keys)
+int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois, const u64 *const *gks,
+                        u64 *const *outs, u32 n);
+size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n);
 // CKKS rescale of n ciphertexts of level m + 1 (on `up`, the context of level
 // m + 1) to level m (on `lo`, the context of level m); ct must not overlap out
 int rescale_impl(fhe_ctx *up, fhe_ctx *lo, const u64 *ct, u64 *out, u32 n);

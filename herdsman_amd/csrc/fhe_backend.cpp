@@ -671,6 +671,33 @@ int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, u
   return FHE_OK;
 }
 
+int fhe_rotate_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                       const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct) {
+  if (!c) return FHE_ERR_INVALID;
+  if (c->params.scheme != FHE_SCHEME_CKKS) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "hoisted rotations are CKKS only");
+  if (c->K == 0) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "context has no special primes (K = 0)");
+  if (n_rot && (!galois || !gks || !outs)) return fhe_fail(c, FHE_ERR_INVALID, "null array");
+  DeviceBind bind(c);
+  const size_t cw = (size_t)2 * c->L * c->n;
+  for (uint32_t r = 0; r < n_rot; ++r) {
+    const uint32_t g = galois[r];
+    if ((g & 1) == 0 || g >= 2 * c->n) return fhe_fail(c, FHE_ERR_INVALID, "galois element must be odd and < 2N");
+    if (n_ct && (!gks[r] || !outs[r] || !ct)) return fhe_fail(c, FHE_ERR_INVALID, "null buffer");
+    // the combine reads c0 through sigma_g: outs must not overlap ct
+    if (n_ct && outs[r] < ct + n_ct * cw && ct < outs[r] + n_ct * cw)
+      return fhe_fail(c, FHE_ERR_INVALID, "hoisted rotation output overlaps its input");
+  }
+  if (!n_ct || !n_rot) return FHE_OK;
+  std::vector<u64 *> o(n_rot);
+  for (uint32_t c0 = 0; c0 < n_ct; c0 += kCtChunk) {
+    const uint32_t m = std::min(kCtChunk, n_ct - c0);
+    for (uint32_t r = 0; r < n_rot; ++r) o[r] = outs[r] + c0 * cw;
+    int rc = rotate_hoisted_impl(c, ct + c0 * cw, n_rot, galois, gks, o.data(), m);
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
 // ---- CKKS levels: the op of the level-m view, its error reported on c
 static int at_level(fhe_ctx *c, uint32_t level, fhe_ctx **v) {
   if (!c) return FHE_ERR_INVALID;
@@ -711,6 +738,14 @@ int fhe_keyswitch_at(fhe_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_
   DeviceBind bind(c);
   int rc = at_level(c, level, &v);
   return rc ? rc : from_view(c, v, fhe_keyswitch(v, d, ksk, out, n));
+}
+
+int fhe_rotate_hoisted_at(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                          const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct, uint32_t level) {
+  fhe_ctx *v;
+  DeviceBind bind(c);
+  int rc = at_level(c, level, &v);
+  return rc ? rc : from_view(c, v, fhe_rotate_hoisted(v, ct, n_rot, galois, gks, outs, n_ct));
 }
 
 int fhe_rescale(fhe_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t level) {

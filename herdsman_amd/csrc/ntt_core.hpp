@@ -105,6 +105,7 @@ struct NttArgs {
   const u64 *e_ext, *e_ksk;
   u32 e_ndig, e_QP;
   u32 e_kQP, e_kshift;  // key rows per digit half; key row of limb i >= L is i + e_kshift (level views)
+  u32 e_ext_g;          // EPI_KSQG / PRO_KSPG: ext is read as sigma_g(ext) (hoisted rotation)
   // PRO_TENSOR (first pass of the inverse NTT of d2 in CKKS mul+relin, poly =
   // ciphertext): the pass reads the operands a, b [ct][2][L][N] instead of d2,
   // writes the relinearisation base out[ct][0] = a0 b0, out[ct][1] = a0 b1 + a1 b0
@@ -157,15 +158,20 @@ namespace {
 // PRO_KSP + d - 1: prologue of the inverse first (row) pass of INTT(acc_P):
 // the P limbs' key-switching inner product over d = 1..4 digits (acc_P is
 // formed at the load positions and never stored)
+// EPI_KSQG / PRO_KSPG + d - 1: the same with the ext words gathered through
+// sigma_g (NttArgs::e_ext_g): the inner product of a hoisted rotation, whose
+// one ModUp of c1 serves every Galois element
 enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, EPI_KSQ = 6, PRO_CONV = 11,
-       PRO_KSP = 16 };
+       PRO_KSP = 16, EPI_KSQG = 21, PRO_KSPG = 26 };
 __host__ __device__ constexpr bool is_conv(int e) { return e >= PRO_CONV && e < PRO_CONV + 4; }
 __host__ __device__ constexpr int conv_ns(int e) { return e - PRO_CONV + 1; }
-__host__ __device__ constexpr bool is_ksq(int e) { return e >= EPI_KSQ && e < EPI_KSQ + 4; }
-__host__ __device__ constexpr int ksq_digits(int e) { return e - EPI_KSQ + 1; }
+__host__ __device__ constexpr bool ksq_gather(int e) { return e >= EPI_KSQG && e < EPI_KSQG + 4; }
+__host__ __device__ constexpr bool is_ksq(int e) { return (e >= EPI_KSQ && e < EPI_KSQ + 4) || ksq_gather(e); }
+__host__ __device__ constexpr int ksq_digits(int e) { return e - (ksq_gather(e) ? EPI_KSQG : EPI_KSQ) + 1; }
 __host__ __device__ constexpr bool is_combine(int e) { return e == EPI_COMBINE || is_ksq(e); }
-__host__ __device__ constexpr bool is_ksp(int e) { return e >= PRO_KSP && e < PRO_KSP + 4; }
-__host__ __device__ constexpr int ksp_digits(int e) { return e - PRO_KSP + 1; }
+__host__ __device__ constexpr bool ksp_gather(int e) { return e >= PRO_KSPG && e < PRO_KSPG + 4; }
+__host__ __device__ constexpr bool is_ksp(int e) { return (e >= PRO_KSP && e < PRO_KSP + 4) || ksp_gather(e); }
+__host__ __device__ constexpr int ksp_digits(int e) { return e - (ksp_gather(e) ? PRO_KSPG : PRO_KSP) + 1; }
 
 // NTT-domain automorphism: slot k holds a(psi^e), e = 2 brv(k) + 1, and
 // sigma_g(a)(psi^e) = a(psi^(e g)); the byte offset of the source slot of k.
@@ -479,9 +485,10 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
 #pragma unroll
         for (int r = 0; r < PD; ++r) {
           const u32 kr = Grp<S, LOGR, 0>::k_reg(r);
+          const u32 eo = ksq_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kr, a.e_ext_g) : voff;
 #pragma unroll
           for (int j = 0; j < KD; ++j) {
-            ek[r][j] = ld_b(ep.kext + j * ep.ext_j + kr, voff);
+            ek[r][j] = ld_b(ep.kext + (ksq_gather(EPI) ? 0 : kr) + j * ep.ext_j, eo);
             ek[r][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
           }
         }
@@ -512,9 +519,10 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
             // the lazy sum below 4q; otherwise it is made canonical.
             if (r + PD < R) {
               const u32 kn = G0::k_reg(r + PD);
+              const u32 eo = ksq_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kn, a.e_ext_g) : voff;
 #pragma unroll
               for (int j = 0; j < KD; ++j) {
-                ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + j * ep.ext_j + kn, voff);
+                ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + (ksq_gather(EPI) ? 0 : kn) + j * ep.ext_j, eo);
                 ek[(r + PD) % (PD + 1)][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
               }
             }
@@ -670,9 +678,10 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 #pragma unroll
       for (int r = 0; r < PD; ++r) {
         const u32 kr = GZ::k_reg(r);
+        const u32 eo = ksp_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kr, a.e_ext_g) : voff;
 #pragma unroll
         for (int j = 0; j < KD; ++j) {
-          ek[r][j] = ld_b(ep.kext + j * ep.ext_j + kr, voff);
+          ek[r][j] = ld_b(ep.kext + (ksp_gather(EPI) ? 0 : kr) + j * ep.ext_j, eo);
           ek[r][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
         }
       }
@@ -680,9 +689,10 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       for (int r = 0; r < R; ++r) {
         if (r + PD < R) {
           const u32 kn = GZ::k_reg(r + PD);
+          const u32 eo = ksp_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kn, a.e_ext_g) : voff;
 #pragma unroll
           for (int j = 0; j < KD; ++j) {
-            ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + j * ep.ext_j + kn, voff);
+            ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + (ksp_gather(EPI) ? 0 : kn) + j * ep.ext_j, eo);
             ek[(r + PD) % (PD + 1)][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
           }
         }

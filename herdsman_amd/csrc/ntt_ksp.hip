@@ -64,7 +64,7 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
 // (ks_inner_kernel) formed in the first (row) pass (PRO_KSP): acc_P is never
 // stored, the P rows of acc receive INTT(acc_P) times d_iscale (ModDown's
 // source constants, as ntt_launch(..., d_iscale) gives them)
-int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig) {
+int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, u32 ext_g) {
   const u32 L = c->L, K = c->K, QP = L + K;
   const size_t N = c->n;
   if (c->log_n <= 14 || ndig < 1 || ndig > 4)
@@ -85,13 +85,18 @@ int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32
     a.e_QP = QP;
     a.e_kQP = ctx_key_qp(c);
     a.e_kshift = c->key_pshift;
+    a.e_ext_g = ext_g & ((2u << c->log_n) - 1);
     const u32 n_jobs = np * K;
     int rc;
-    switch (ndig) {
+    switch (ndig + (ext_g ? 4 : 0)) {
       case 1: rc = row_pass<PRO_KSP>(c, a, true, n_jobs); break;
       case 2: rc = row_pass<PRO_KSP + 1>(c, a, true, n_jobs); break;
       case 3: rc = row_pass<PRO_KSP + 2>(c, a, true, n_jobs); break;
-      default: rc = row_pass<PRO_KSP + 3>(c, a, true, n_jobs); break;
+      case 4: rc = row_pass<PRO_KSP + 3>(c, a, true, n_jobs); break;
+      case 5: rc = row_pass<PRO_KSPG>(c, a, true, n_jobs); break;
+      case 6: rc = row_pass<PRO_KSPG + 1>(c, a, true, n_jobs); break;
+      case 7: rc = row_pass<PRO_KSPG + 2>(c, a, true, n_jobs); break;
+      default: rc = row_pass<PRO_KSPG + 3>(c, a, true, n_jobs); break;
     }
     if (rc) return rc;
     if ((rc = ntt_col_plain(c, a, true, n_jobs))) return rc;

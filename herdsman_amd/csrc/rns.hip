@@ -811,10 +811,12 @@ static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
 //         base may alias out (element-wise).
 //   base_g (NTT form with the fused ModDown only): base_b is read as
 //         sigma_g(base_b); base must not overlap out.
-static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
-                         bool ntt_form, bool dc_is_coef = false, u32 base_g = 0) {
+// Split in two for hoisted rotations: ks_extend (steps 1-3: INTT, ModUp, NTT of
+// the converted limbs, into w.ext) runs once per input, ks_finish (steps 4-6:
+// inner product, ModDown) once per key.
+static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is_coef) {
   const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
-  u64 *dc = w.dc, *ext = w.ext, *acc = w.acc, *conv = w.conv;
+  u64 *dc = w.dc, *ext = w.ext;
   int rc;
   // CKKS at two-pass sizes: ModUp runs inside the column pass of the NTT of
   // its outputs (ntt_fwd_modup_launch); dc then holds ModUp's scaled sources
@@ -840,6 +842,22 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
     // (< 8q) NTT outputs as they are, so the last pass skips canonicalising
     if ((rc = ntt_launch(c, m, false, false, c->special))) return rc;
   }
+  (void)K;
+  return FHE_OK;
+}
+
+// ext_g (NTT form, fused ModDown, at most 4 digits only): the inner product
+// reads ext as sigma_g(ext) (EPI_KSQG / PRO_KSPG)
+static bool ks_fused_inner(const fhe_ctx *c, u32 ndig, bool ntt_form) {
+  return ntt_form && c->fuse_moddown && ndig <= 4 && KSP_FUSE;
+}
+static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, const u64 *base, u64 *out, u32 n,
+                     u32 add_mask, bool ntt_form, u32 base_g, u32 ext_g) {
+  const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
+  u64 *acc = w.acc, *conv = w.conv;
+  int rc;
+  if (ext_g && !ks_fused_inner(c, ndig, ntt_form))
+    return fhe_fail(c, FHE_ERR_UNSUPPORTED, "gathered key-switch input without the fused inner product");
   // 4. inner product with the key.  With the fused ModDown and at most 4
   //    digits, the Q limbs' inner product runs inside the last pass of
   //    NTT(conv) (EPI_KSQ), so only the P limbs (ModDown's sources) are formed
@@ -854,11 +872,11 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   //      conversion in its first pass and the combine in its last
   //      (out = base + (acc_Q - conv) P^-1): conv never makes an HBM round trip
   if (ntt_form && c->fuse_moddown) {
-    if (ksq && KSP_FUSE) rc = ntt_inv_ksp_launch(c, acc, ext, ksk, n, ndig);
+    if (ksq && KSP_FUSE) rc = ntt_inv_ksp_launch(c, acc, ext, ksk, n, ndig, ext_g);
     else rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale);
     if (rc) return rc;
     return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, &c->moddown, ksq ? ext : nullptr,
-                                  ksk, ndig, base_g);
+                                  ksk, ndig, base_g, nullptr, nullptr, ext_g);
   }
   if (base_g) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated key-switch base without the fused ModDown");
   // 5. ModDown: INTT the P part (all of Q u P for BFV), convert P -> Q
@@ -869,6 +887,12 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   // 6. combine: fused into the last pass of NTT(conv) for NTT-form results
   if (ntt_form) return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask);
   return SP_DISPATCH(c, combine_impl, c, acc, conv, base, out, n, add_mask);
+}
+
+static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
+                         bool ntt_form, bool dc_is_coef = false, u32 base_g = 0) {
+  int rc = ks_extend(c, w, n, ntt_form, dc_is_coef);
+  return rc ? rc : ks_finish(c, w, w.ext, ksk, base, out, n, add_mask, ntt_form, base_g, 0);
 }
 
 // Hybrid key switching of an arbitrary input d ([n][d_stride limbs], the L
@@ -914,6 +938,79 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
   return keyswitch_run(c, w, gk, base, out, n, 1u, ntt_form);
 }
 
+
+// NTT-domain automorphism of whole rows: dst row r = sigma_g(src row r), rows
+// taken rpg at a time from groups src_gs / dst_gs rows apart (the hoisted
+// rotation's generic path: sigma_g on the ModUp output and on c0)
+__global__ void __launch_bounds__(EW_BLOCK) aut_rows_kernel(const u64 *__restrict__ src, u32 src_gs,
+                                                            u64 *__restrict__ dst, u32 dst_gs, u32 rpg, u32 g,
+                                                            u32 log_n) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x, r = blockIdx.y;
+  const size_t N = (size_t)1 << log_n, grp = r / rpg, i = r % rpg;
+  const u32 mask = (2u << log_n) - 1;
+  const u32 e = 2 * (__brev(k) >> (32 - log_n)) + 1;
+  const u32 e2 = (u32)(((u64)e * g) & mask);
+  const u32 sk = __brev((e2 - 1) >> 1) >> (32 - log_n);
+  dst[(grp * dst_gs + i) * N + k] = src[(grp * src_gs + i) * N + sk];
+}
+static int aut_rows(fhe_ctx *c, const u64 *src, u32 src_gs, u64 *dst, u32 dst_gs, u32 rpg, u32 n_rows, u32 g) {
+  const u32 per = kMaxGridY / rpg * rpg;
+  const size_t N = c->n;
+  for (u32 r0 = 0; r0 < n_rows; r0 += per) {
+    const u32 nr = std::min(per, n_rows - r0), g0 = r0 / rpg;
+    hipLaunchKernelGGL(aut_rows_kernel, dim3(c->n / EW_BLOCK, nr), dim3(EW_BLOCK), 0, c->stream,
+                       src + (size_t)g0 * src_gs * N, src_gs, dst + (size_t)g0 * dst_gs * N, dst_gs, rpg, g, c->log_n);
+    int rc = fhe_check(c, hipGetLastError(), "aut_rows_kernel");
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
+size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n) {
+  const size_t N = c->n, L = c->L, QP = c->L + c->K, ndig = (c->L + c->alpha - 1) / c->alpha;
+  return keyswitch_ws_bytes(c, n) + sizeof(u64) * N * n * (ndig * QP + 2 * L);
+}
+
+// Hoisted rotations (CKKS; oracle orc_rotate_hoisted, OpenFHE EvalFastRotation):
+// c1 is extended ONCE (INTT, ModUp, NTT of the converted limbs), then every
+// Galois element g_r key-switches sigma_g(ext) -- not ModUp(sigma_g(c1)), so the
+// bits differ from rotate_impl's by the ModUp error term -- and adds sigma_g(c0).
+// Two-pass sizes with the fused inner product: sigma_g is a gather inside the
+// inner-product passes (EPI_KSQG / PRO_KSPG) and the combine reads c0 through
+// sigma_g, so a rotation costs its key switch's inner product and ModDown only.
+// Otherwise sigma_g(ext) and sigma_g(c0) are materialised (aut_rows_kernel).
+// outs[r] must not overlap ct.
+int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois, const u64 *const *gks,
+                        u64 *const *outs, u32 n) {
+  const size_t LN = (size_t)c->L * c->n, QP = c->L + c->K;
+  void *ws;
+  int rc = ctx_workspace(c, rotate_hoisted_ws_bytes(c, n), &ws);
+  if (rc) return rc;
+  const KsWs w = ks_layout(c, n, (u64 *)ws);
+  u64 *ext_g = w.conv + n * 2 * LN;      // [n][ndig][QP][N] (generic path)
+  u64 *base = ext_g + n * w.ndig * QP * c->n;  // [n][2][L][N], poly 0 = sigma(c0) (generic path)
+  const bool gather = c->log_n > 14 && ks_fused_inner(c, w.ndig, true);
+  if (c->log_n > 14) {
+    // the identity automorphism: INTT(c1) with the ModUp source scaling and
+    // the own-digit slots c1 R, as rotate_impl's fused prologue
+    if ((rc = ntt_inv_automorph_launch(c, ct, 1u, nullptr, w.dc, w.ext, n, w.ndig))) return rc;
+  } else if ((rc = SP_DISPATCH(c, ks_prep_impl, c, ct + LN, 2 * c->L, w.dc, w.ext, n, w.ndig))) {
+    return rc;
+  }
+  if ((rc = ks_extend(c, w, n, true, c->log_n > 14))) return rc;
+  for (u32 r = 0; r < n_rot; ++r) {
+    const u32 g = galois[r];
+    if (gather) {
+      rc = ks_finish(c, w, w.ext, gks[r], ct, outs[r], n, 1u, true, g, g);
+    } else {
+      if ((rc = aut_rows(c, w.ext, w.ndig * QP, ext_g, w.ndig * QP, w.ndig * QP, n * w.ndig * QP, g))) return rc;
+      if ((rc = aut_rows(c, ct, 2 * c->L, base, 2 * c->L, c->L, n * c->L, g))) return rc;
+      rc = ks_finish(c, w, ext_g, gks[r], base, outs[r], n, 1u, true, 0, 0);
+    }
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
 
 // ------------------------------------------------------------ CKKS rescale
 size_t rescale_ws_bytes(const fhe_ctx *lo, u32 n) { return sizeof(u64) * lo->n * 2 * (size_t)n * (1 + lo->L); }

@@ -142,6 +142,16 @@ int fhe_keyswitch(fhe_ctx *ctx, const uint64_t *d, const uint64_t *ksk, uint64_t
 /* automorphism X -> X^galois_elt followed by key switching with the Galois key */
 int fhe_rotate(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const uint64_t *gk, uint64_t *out,
                uint32_t n_ct);
+/* hoisted rotations (CKKS): n_rot Galois elements applied to the same n_ct
+ * ciphertexts, c1's ModUp computed once (OpenFHE EvalFastRotationPrecompute +
+ * EvalFastRotation, which herdsman's linked library provides for rotation-heavy
+ * circuits).  galois_elts, gks, outs: HOST arrays of n_rot entries; gks[r] is a
+ * device Galois key for galois_elts[r], outs[r] a device [n_ct][2][L][N]
+ * buffer that must not overlap ct.  outs[r] = (sigma(c0) + KS_0, KS_1) with KS
+ * over sigma_g(ModUp(c1)): decrypts like fhe_rotate's result, but the bits
+ * differ from it by the ModUp error term (oracle orc_rotate_hoisted). */
+int fhe_rotate_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
+                       const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct);
 /* 5^steps mod 2N (steps may be negative); conjugation is 2N-1 */
 int fhe_galois_elt(const fhe_ctx *ctx, int32_t steps, uint32_t *out);
 
@@ -163,6 +173,8 @@ int fhe_rotate_at(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const u
                   uint32_t n_ct, uint32_t level);
 int fhe_keyswitch_at(fhe_ctx *ctx, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
                      uint32_t level);
+int fhe_rotate_hoisted_at(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
+                          const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct, uint32_t level);
 /* CKKS rescale, level -> level - 1 (2 <= level <= L): out [n_ct][2][level-1][N]
  * = round(ct / q_{level-1}) -- OpenFHE DCRTPoly::DropLastElementAndScale /
  * SEAL divide_and_round_q_last_ntt (the dropped limb lifted centrally).

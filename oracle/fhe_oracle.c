@@ -862,9 +862,9 @@ void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t
  * outs[r] = (sigma(c0) + KS0, KS1) with KS over sigma_g(ModUp(c1)) and key
  * gks[r] -- one ModUp of c1 serves every rotation.  gks [n_rot][key],
  * outs [n_rot][n_ct][2][L][N]. */
-void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
-                        const uint64_t *gks, uint64_t *outs, uint32_t n_ct) {
-  const size_t L = c->L, N = c->n, CT = 2 * L * N, KW = (size_t)c->dnum * 2 * (c->L + c->K) * N;
+static void rotate_hoisted_lvl(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                               const uint64_t *gks, uint64_t *outs, uint32_t n_ct, uint32_t lvl) {
+  const size_t L = lvl, N = c->n, CT = 2 * L * N, KW = (size_t)c->dnum * 2 * (c->L + c->K) * N;
   for (uint32_t r = 0; r < n_rot; ++r) {
 #pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
     for (long i = 0; i < (long)n_ct; ++i) {
@@ -877,6 +877,17 @@ void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, co
       free(ks);
     }
   }
+}
+
+void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                        const uint64_t *gks, uint64_t *outs, uint32_t n_ct) {
+  rotate_hoisted_lvl(c, ct, n_rot, galois, gks, outs, n_ct, c->L);
+}
+
+/* the same at level lvl: ct, outs [..][2][lvl][N], full-level keys */
+void orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                           const uint64_t *gks, uint64_t *outs, uint32_t n_ct, uint32_t lvl) {
+  rotate_hoisted_lvl(c, ct, n_rot, galois, gks, outs, n_ct, lvl);
 }
 
 /* ------------------------------------------------- CKKS levels (rescale) */

@@ -95,6 +95,8 @@ uint32_t orc_galois_elt(const orc_ctx *c, int32_t steps);
  * gks [n_rot][dnum][2][L+K][N]; KS over sigma_g(ModUp(c1)) (one ModUp for all) */
 void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                         const uint64_t *gks, uint64_t *outs, uint32_t n_ct);
+void orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                           const uint64_t *gks, uint64_t *outs, uint32_t n_ct, uint32_t lvl);
 
 /* ---- CKKS levels: ciphertexts [n_ct][2][lvl][N] with the first lvl Q primes
  * (1 <= lvl <= L).  Key switching at level lvl uses the full-level key's rows

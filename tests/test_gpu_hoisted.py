@@ -1,0 +1,126 @@
+"""Hoisted CKKS rotations on the HIP backend (fhe_rotate_hoisted[_at]): one
+ModUp of c1 shared by every Galois element, sigma_g applied to the extension
+(OpenFHE EvalFastRotationPrecompute / EvalFastRotation; oracle
+orc_rotate_hoisted, oracle/bigint_model.py rotate_hoisted).
+
+Evidence:
+  * the big-int golden fixture ckks_hoisted_n1024_l5.npz (one-pass size: the
+    generic path that materialises sigma_g(ext) and sigma_g(c0));
+  * the CPU oracle on identical seeded inputs at the metric parameters
+    N=2^16, L=12, K=4, dnum=3 (the fused path: sigma_g is a gather inside the
+    inner-product passes) at levels 12, 7 (partial last digit) and 5;
+  * N=2^15 with dnum=5 (more digits than the fused inner product takes: the
+    generic path at a two-pass size) and OpenFHE-style generic primes.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle_ffi import Oracle, SCHEME_BFV, SCHEME_CKKS
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def hb():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    import herdsman_amd.backend as hb
+
+    hb.load_library()
+    return hb
+
+
+@pytest.fixture(scope="module")
+def metric(hb):
+    o = Oracle(SCHEME_CKKS, 16, 12, 4, 3)
+    c = hb.Context(SCHEME_CKKS, 16, 12, 4, 3, moduli=o.moduli)
+    return o, c
+
+
+def _run(hb, c, ct, gs, gks, lvl=None):
+    n = ct.shape[0]
+    shape = (n, 2, ct.shape[2], c.n)
+    outs = [hb.empty(shape) for _ in gs]
+    d_ct = hb.to_device(ct)
+    d_gk = [hb.to_device(k) for k in gks]
+    if lvl is None:
+        c.rotate_hoisted(d_ct, gs, d_gk, outs)
+    else:
+        c.rotate_hoisted_at(d_ct, gs, d_gk, outs, lvl)
+    return np.stack([hb.to_host(o) for o in outs])
+
+
+def test_hoisted_golden(hb):
+    g = np.load(os.path.join(GOLD, "ckks_hoisted_n1024_l5.npz"))
+    c = hb.Context(SCHEME_CKKS, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), moduli=g["moduli"])
+    got = _run(hb, c, g["ct"][None], [int(x) for x in g["galois"]], list(g["gks"]))
+    assert np.array_equal(got[:, 0], g["out"])
+
+
+def test_hoisted_metric_params(hb, metric):
+    o, c = metric
+    ct = o.uniform((2, 2, o.L, o.n), seed=1100)
+    gs = [o.galois_elt(1), o.galois_elt(-7), 2 * o.n - 1]
+    gks = [o.uniform(o.key_shape(), seed=1101 + i) for i in range(len(gs))]
+    want = o.rotate_hoisted(ct, gs, np.stack(gks))
+    got = _run(hb, c, ct, gs, gks)
+    assert np.array_equal(got, want)
+    # one Galois element: the hoisted result differs from the plain rotation
+    # only by the ModUp error term, so it is a distinct (but valid) ciphertext
+    plain = o.rotate(ct[:1], gs[0], gks[0])
+    assert not np.array_equal(plain, want[0, :1])
+
+
+@pytest.mark.parametrize("lvl", [7, 5])
+def test_hoisted_at_levels(hb, metric, lvl):
+    o, c = metric
+    ct = o.uniform((1, 2, lvl, o.n), seed=1200 + lvl)
+    gs = [o.galois_elt(3), o.galois_elt(-1)]
+    gks = [o.uniform(o.key_shape(), seed=1210 + i) for i in range(len(gs))]
+    want = o.rotate_hoisted_at(ct, gs, np.stack(gks), lvl)
+    assert np.array_equal(_run(hb, c, ct, gs, gks, lvl), want)
+
+
+def test_hoisted_many_digits_generic_primes(hb):
+    """dnum = 5 > 4 digits at N = 2^15: sigma_g(ext) is materialised; generic
+    (OpenFHE-style) primes take the generic Montgomery path."""
+    from herdsman_amd.params import openfhe_style_primes
+    mods = openfhe_style_primes([(55, 5), (61, 5), (61, 2)], 15)
+    o = Oracle(SCHEME_CKKS, 15, 10, 2, 5, moduli=mods)
+    c = hb.Context(SCHEME_CKKS, 15, 10, 2, 5, moduli=o.moduli)
+    ct = o.uniform((1, 2, o.L, o.n), seed=1300)
+    gs = [o.galois_elt(2), o.galois_elt(-5)]
+    gks = [o.uniform(o.key_shape(), seed=1301 + i) for i in range(len(gs))]
+    assert np.array_equal(_run(hb, c, ct, gs, gks), o.rotate_hoisted(ct, gs, np.stack(gks)))
+
+
+def test_hoisted_errors(hb, metric):
+    o, c = metric
+    lib = hb.load_library()
+    import ctypes as C
+    ct = hb.empty((1, 2, o.L, o.n))
+    k = hb.empty(o.key_shape())
+    ga = (C.c_uint32 * 1)(o.galois_elt(1))
+    ka = (C.c_uint64 * 1)(hb._ptr(k))
+    oa = (C.c_uint64 * 1)(hb._ptr(ct))  # output == input
+    assert lib.fhe_rotate_hoisted(c.h, hb._ptr(ct), 1, C.addressof(ga), C.addressof(ka), C.addressof(oa), 1) \
+        == hb.FHE_ERR_INVALID
+    out = hb.empty((1, 2, o.L, o.n))
+    oa[0] = hb._ptr(out)
+    ga[0] = 4  # even
+    assert lib.fhe_rotate_hoisted(c.h, hb._ptr(ct), 1, C.addressof(ga), C.addressof(ka), C.addressof(oa), 1) \
+        == hb.FHE_ERR_INVALID
+    assert lib.fhe_rotate_hoisted(c.h, hb._ptr(ct), 0, None, None, None, 1) == hb.FHE_OK
+    bfv = hb.Context(SCHEME_BFV, 12, 3, 1, 1, t=65537)
+    z = hb.empty((1, 2, 3, bfv.n))
+    kz = hb.empty(bfv.key_shape())
+    ka[0] = hb._ptr(kz)
+    oa[0] = hb._ptr(hb.empty((1, 2, 3, bfv.n)))
+    ga[0] = 5
+    assert lib.fhe_rotate_hoisted(bfv.h, hb._ptr(z), 1, C.addressof(ga), C.addressof(ka), C.addressof(oa), 1) \
+        == hb.FHE_ERR_UNSUPPORTED

@@ -136,3 +136,4 @@ def test_ckks_hoisted_rotations_golden():
     o = Oracle(SCHEME_CKKS, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), moduli=g["moduli"])
     out = o.rotate_hoisted(g["ct"][None], g["galois"], g["gks"])
     assert np.array_equal(out[:, 0], g["out"])
+    assert np.array_equal(o.rotate_hoisted_at(g["ct"][None], g["galois"], g["gks"], o.L)[:, 0], g["out"])

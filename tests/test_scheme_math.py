@@ -115,3 +115,27 @@ def test_ckks_hoisted_rotations_decrypt():
         dec = crt_centered(o.decrypt(outs[r, 0], s_qp), Q)
         want = [delta * v for v in automorph_int(u, g)]
         assert max(abs(a - b) for a, b in zip(dec, want)) < 2 ** 30
+
+
+def test_ckks_hoisted_rotations_at_level_decrypt():
+    """The same at a reduced level (3 of 4 limbs: a partial last digit) with the
+    full-level Galois keys."""
+    o = Oracle(SCHEME_CKKS, 10, 4, 2, 2)
+    lvl = 3
+    Q = [int(q) for q in o.moduli[:lvl]]
+    s, s_qp = _keys(o)
+    rng = random.Random(8)
+    delta = 1 << 40
+    u = [rng.randint(-100, 100) for _ in range(o.n)]
+    ct = o.encrypt(to_rns([delta * x for x in u], [int(q) for q in o.moduli[:o.L]]), s_qp, 808)
+    ct = np.ascontiguousarray(ct[:, :lvl])
+    gs = [o.galois_elt(k) for k in (2, -1)]
+    gks = np.stack([o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=40 + i) for i, g in enumerate(gs)])
+    outs = o.rotate_hoisted_at(ct[None], gs, gks, lvl)
+    qs = o.moduli[:lvl].astype(object)[:, None]
+    for r, g in enumerate(gs):
+        c0, c1 = outs[r, 0]
+        m = ((c0.astype(object) + c1.astype(object) * s_qp[:lvl].astype(object)) % qs).astype(np.uint64)
+        dec = crt_centered(o.ntt_inv(m[None])[0], Q)
+        want = [delta * v for v in automorph_int(u, g)]
+        assert max(abs(a - b) for a, b in zip(dec, want)) < 2 ** 30
