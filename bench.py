@@ -551,7 +551,8 @@ def _timed(fn, reps, stream):
 
 def secondary_configs(hb, ctx, gk, a, b, out, dev, stream, B, reps):
     """Per-GPU throughput of the other BASELINE.json configs (same synthetic-data rules):
-    C4 CKKS rotate + hybrid KS at the metric parameters (B ciphertexts per call),
+    C4 CKKS rotate + hybrid KS at the metric parameters (B ciphertexts per call) and
+    4 hoisted rotations of the same batch (fhe_rotate_hoisted, one ModUp of c1),
     C3 BFV mul+relin at N=2^15 L=8 (BEHZ), C2 forward+inverse NTT at N=2^14 L=4, and
     the metric op on OpenFHE-style primes (q = 1 mod 2N, generic Montgomery path)
     next to the same single-context call on the default primes."""
@@ -562,6 +563,13 @@ def secondary_configs(hb, ctx, gk, a, b, out, dev, stream, B, reps):
     ct, o = a[:B], out[:B]
     t = _timed(lambda: ctx.rotate(ct, g, gk, o), reps, stream)
     res["C4_ckks_rotate_per_s"] = round(B / t, 1)
+    # hoisted: 4 Galois elements over the same B ciphertexts, one ModUp of c1
+    # (rotations per second = 4 B / t; the same key stands in for the 4 keys)
+    gs = [ctx.galois_elt(s) for s in (1, 2, -1, 5)]
+    hos = [hb.empty((B, 2, L, 1 << LOG_N), device=dev) for _ in gs]
+    t = _timed(lambda: ctx.rotate_hoisted(ct, gs, [gk] * len(gs), hos), reps, stream)
+    res["C4_ckks_rotate_hoisted4_rot_per_s"] = round(len(gs) * B / t, 1)
+    del hos
     t = _timed(lambda: ctx.mul_relin(ct, b[:B], gk, o), reps, stream)
     res["C5_mul_relin_1ctx_per_s"] = round(B / t, 1)
     # the CKKS multiply as a circuit runs it: mul+relin then rescale (12 -> 11 limbs),

@@ -670,7 +670,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       // generic), the running sum is kept below 2q.  Operands software-
       // pipelined PD elements deep (as EPI_KSQ)
       constexpr int KD = ksp_digits(EPI);
-      constexpr int PD = SP ? KSP_PD : 1;
+      constexpr int PD = SP || ksp_gather(EPI) ? KSP_PD : 1;
       u64 nq1 = 0 - mi.q, nq2 = 0 - 2 * mi.q;
       asm("" : "+s"(nq1));
       asm("" : "+s"(nq2));
