@@ -610,7 +610,7 @@ void GpuWorkerGroup::completion_loop() {
 // ------------------------------------------------------------- evaluation
 namespace {
 
-enum class Op : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4, RESCALE = 5 };
+enum class Op : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4, RESCALE = 5, ROTSUM = 6 };
 struct Instr {
   Op op;
   int32_t arg;
@@ -627,7 +627,7 @@ std::vector<Instr> lower_circuit(const C &c) {
     std::vector<Instr> out;
     for (const auto &i : c.program) {
       const uint32_t op = static_cast<uint32_t>(i.op);
-      if (op > static_cast<uint32_t>(Op::RESCALE)) throw std::runtime_error("unknown circuit op");
+      if (op > static_cast<uint32_t>(Op::ROTSUM)) throw std::runtime_error("unknown circuit op");
       out.push_back(Instr{static_cast<Op>(op), static_cast<int32_t>(i.arg)});
     }
     return out;
@@ -841,6 +841,44 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
         const uint32_t m = stack.back().level;
         StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
         ck(s.ctx, fhe_rotate_at(s.ctx, stack.back().buf.p, g, gk.p, o.buf.p, (uint32_t)n, m), "rotate");
+        stack.back() = std::move(o);
+        break;
+      }
+      case Op::ROTSUM: {
+        // sum of hoisted rotations: one fhe_rotate_hoisted_at over every step
+        // in the mask, then the adds (bit 0 adds the input itself)
+        if (stack.empty()) throw std::runtime_error("circuit stack underflow");
+        if (s.scheme != FHE_SCHEME_CKKS) throw std::runtime_error("rotsum is CKKS only");
+        const uint32_t mask = (uint32_t)ins.arg;
+        if (mask == 0 || (mask >> 31)) throw std::runtime_error("rotsum step mask must be in [1, 2^31)");
+        const uint32_t m = stack.back().level;
+        std::vector<uint32_t> gs;
+        std::vector<const uint64_t *> gks;
+        std::vector<ArenaBuf> outs;
+        std::vector<uint64_t *> outp;
+        for (int32_t k = 1; k < 31; ++k) {
+          if (!((mask >> k) & 1)) continue;
+          uint32_t g = 0;
+          gks.push_back(galois_key(s, ks, k, &g).p);
+          gs.push_back(g);
+          outs.emplace_back(*ls.arena, s.ct_words(m) * n);
+          outp.push_back(outs.back().p);
+        }
+        const uint64_t *top = stack.back().buf.p;
+        if (!gs.empty())
+          ck(s.ctx, fhe_rotate_hoisted_at(s.ctx, top, (uint32_t)gs.size(), gs.data(), gks.data(), outp.data(),
+                                          (uint32_t)n, m), "rotate_hoisted");
+        if (outs.empty()) break;  // mask 1: the input itself
+        if (outs.size() == 1 && !(mask & 1)) {
+          stack.back() = StackCt{std::move(outs[0]), m};
+          break;
+        }
+        StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
+        size_t first = 0;
+        const uint64_t *acc = top;
+        if (!(mask & 1)) acc = outp[first++];
+        for (size_t r = first; r < outp.size(); ++r, acc = o.buf.p)
+          ck(s.ctx, fhe_add_at(s.ctx, acc, outp[r], o.buf.p, (uint32_t)n, m), "rotsum add");
         stack.back() = std::move(o);
         break;
       }

@@ -55,10 +55,13 @@ struct CryptoKeyPtr {
 // Stand-in circuit: a stack program over the ciphertexts of one row.
 // CKKS operands may sit at different levels: binary ops run at the lower one
 // (the other operand's extra limbs dropped), RESCALE drops one level.
-enum class CtOp : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4, RESCALE = 5 };
+// ROTSUM (CKKS) replaces the top with sum_{i in arg} rot_i(top), arg a bit mask
+// of step counts 0..30 (bit 0: the ciphertext itself), the rotations hoisted
+// (one ModUp of c1 for all of them: a baby-step block of a linear transform).
+enum class CtOp : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4, RESCALE = 5, ROTSUM = 6 };
 struct CircuitInstr {
   CtOp op;
-  int32_t arg = 0;  // PUSH_INPUT: index of the ciphertext in the row; ROTATE: steps
+  int32_t arg = 0;  // PUSH_INPUT: index of the ciphertext in the row; ROTATE: steps; ROTSUM: step mask
 };
 struct Circuit {
   std::vector<CircuitInstr> program;

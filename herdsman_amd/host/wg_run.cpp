@@ -84,6 +84,19 @@ static herd::common::Circuit parse_program(int argc, char **argv, int first) {
     else if (t == "mul") c.program.push_back({CtOp::MUL_RELIN, 0});
     else if (t.rfind("rot:", 0) == 0) c.program.push_back({CtOp::ROTATE, std::stoi(t.substr(4))});
     else if (t == "rescale") c.program.push_back({CtOp::RESCALE, 0});
+    else if (t.rfind("rotsum:", 0) == 0) {  // rotsum:0,1,2,4 -> step mask
+      int32_t mask = 0;
+      std::string v = t.substr(7);
+      for (size_t p0 = 0; p0 < v.size();) {
+        size_t p1 = v.find(',', p0);
+        if (p1 == std::string::npos) p1 = v.size();
+        const int k = std::stoi(v.substr(p0, p1 - p0));
+        if (k < 0 || k > 30) throw std::runtime_error("rotsum steps must be in [0, 30]");
+        mask |= 1 << k;
+        p0 = p1 + 1;
+      }
+      c.program.push_back({CtOp::ROTSUM, mask});
+    }
     else throw std::runtime_error("unknown program token " + t);
   }
   return c;

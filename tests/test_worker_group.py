@@ -167,6 +167,37 @@ def test_gpu_map_task_mul_rotate(wg_run, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("log_n,steps,lvl", [(16, (0, 1, 3), 11), (12, (1, 2), 4)])
+def test_gpu_map_task_rotsum_hoisted(wg_run, tmp_path, log_n, steps, lvl):
+    """ROTSUM: the sum of the input's rotations by the given steps (0 = the input
+    itself), the rotations hoisted (fhe_rotate_hoisted_at: one ModUp of c1);
+    at N=2^16 on level-11 rows (the fused gather path at a reduced level), at
+    N=2^12 after a product (the generic path)."""
+    from oracle_ffi import SCHEME_CKKS
+    L, K, dnum = (12, 4, 3) if log_n == 16 else (4, 2, 2)
+    o, storage, keys = _setup(tmp_path, SCHEME_CKKS, log_n, L, K, dnum)
+    rows = 2
+    a = o.uniform((rows, 2, lvl, o.n), seed=61)
+    b = o.uniform((rows, 2, lvl, o.n), seed=62)
+    rlk = o.uniform(o.key_shape(), seed=63)
+    rot = [k for k in steps if k]
+    gs = [o.galois_elt(k) for k in rot]
+    gks = [o.uniform(o.key_shape(), seed=70 + k) for k in rot]
+    write_partition(os.path.join(storage, "sr", "fa", "0"), [ct_row(o, [a[i], b[i]]) for i in range(rows)])
+    write_keys(os.path.join(keys, "sr", "0.key"), o, rlk, dict(zip(gs, gks)))
+    prog = ["in0"] if log_n == 16 else ["in0", "in1", "mul"]
+    r = subprocess.run([wg_run, "map", storage, keys, "sr", "0", params_arg(o, str(tmp_path)), "fa", "0", "fb"]
+                       + prog + ["rotsum:" + ",".join(map(str, steps))], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.stack([parse_row(o, p, level=lvl) for p in read_partition(os.path.join(storage, "sr", "fb", "0"))])
+    x = a if log_n == 16 else o.mul_relin_at(a, b, rlk, lvl)
+    terms = list(o.rotate_hoisted_at(x, gs, np.stack(gks), lvl)) + ([x] if 0 in steps else [])
+    qs = o.moduli[:lvl].astype(object)[None, None, :, None]
+    want = sum(t.astype(object) for t in terms) % qs
+    assert np.array_equal(got, want.astype(np.uint64))
+
+
+@pytest.mark.gpu
 def test_gpu_map_task_ckks_levels(wg_run, tmp_path):
     """A depth-2 CKKS circuit through the worker group: rows carry ciphertexts at
     levels 12, 12 and 11; in0 in1 mul rescale in1 mul in2 add rescale runs the
