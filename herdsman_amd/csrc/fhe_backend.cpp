@@ -472,6 +472,7 @@ int fhe_reserve(fhe_ctx *c, uint32_t max_batch) {
   max_batch = std::min(max_batch, kCtChunk);  // ops run in passes of at most kCtChunk ciphertexts
   size_t need = (size_t)sizeof(u64) * c->n * max_batch * 2 * c->L;  // rotate / mul scratch
   if (c->K) need += keyswitch_ws_bytes(c, max_batch);
+  if (c->K && c->params.scheme == FHE_SCHEME_CKKS) need = std::max(need, rotate_hoisted_ws_bytes(c, max_batch));
   if (c->nB) need = std::max(need, bfv_mul_ws_bytes(c, max_batch));
   void *p;
   return ctx_workspace(c, need, &p);

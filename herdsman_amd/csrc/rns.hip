@@ -966,9 +966,14 @@ static int aut_rows(fhe_ctx *c, const u64 *src, u32 src_gs, u64 *dst, u32 dst_gs
   return FHE_OK;
 }
 
+// the gather path (sigma_g inside the fused inner-product passes) needs only
+// the key-switch scratch; the generic one also sigma_g(ext) and sigma_g(c0)
+static bool hoisted_gather(const fhe_ctx *c) {
+  return c->log_n > 14 && ks_fused_inner(c, (c->L + c->alpha - 1) / c->alpha, true);
+}
 size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n) {
   const size_t N = c->n, L = c->L, QP = c->L + c->K, ndig = (c->L + c->alpha - 1) / c->alpha;
-  return keyswitch_ws_bytes(c, n) + sizeof(u64) * N * n * (ndig * QP + 2 * L);
+  return keyswitch_ws_bytes(c, n) + (hoisted_gather(c) ? 0 : sizeof(u64) * N * n * (ndig * QP + 2 * L));
 }
 
 // Hoisted rotations (CKKS; oracle orc_rotate_hoisted, OpenFHE EvalFastRotation):
@@ -989,7 +994,7 @@ int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois,
   const KsWs w = ks_layout(c, n, (u64 *)ws);
   u64 *ext_g = w.conv + n * 2 * LN;      // [n][ndig][QP][N] (generic path)
   u64 *base = ext_g + n * w.ndig * QP * c->n;  // [n][2][L][N], poly 0 = sigma(c0) (generic path)
-  const bool gather = c->log_n > 14 && ks_fused_inner(c, w.ndig, true);
+  const bool gather = hoisted_gather(c);
   if (c->log_n > 14) {
     // the identity automorphism: INTT(c1) with the ModUp source scaling and
     // the own-digit slots c1 R, as rotate_impl's fused prologue

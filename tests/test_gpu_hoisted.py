@@ -124,3 +124,15 @@ def test_hoisted_errors(hb, metric):
     ga[0] = 5
     assert lib.fhe_rotate_hoisted(bfv.h, hb._ptr(z), 1, C.addressof(ga), C.addressof(ka), C.addressof(oa), 1) \
         == hb.FHE_ERR_UNSUPPORTED
+
+
+def test_hoisted_chunked_batch(hb):
+    """More ciphertexts than one internal pass (kCtChunk = 512): the outputs of
+    every chunk land at their own offsets."""
+    o = Oracle(SCHEME_CKKS, 12, 3, 2, 3)
+    c = hb.Context(SCHEME_CKKS, 12, 3, 2, 3, moduli=o.moduli)
+    ct = o.uniform((520, 2, o.L, o.n), seed=1400)
+    gs = [o.galois_elt(1), o.galois_elt(-2)]
+    gks = [o.uniform(o.key_shape(), seed=1401 + i) for i in range(len(gs))]
+    c.reserve(520)
+    assert np.array_equal(_run(hb, c, ct, gs, gks), o.rotate_hoisted(ct, gs, np.stack(gks)))
