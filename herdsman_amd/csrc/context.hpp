@@ -81,6 +81,12 @@ struct fhe_ctx {
   u64 *d_iscale = nullptr;     // [nmod]
   bool fuse_moddown = false;
   bool fuse_modup = false;     // also alpha <= 4
+  // BFV relinearisation at two-pass sizes (alpha, K, digits <= 4): ModUp in the
+  // NTT column pass, the inner product in INTT(acc)'s first pass, ModDown and
+  // the combine in one coefficient-domain kernel (bfv_ks_fused)
+  bool bfv_ks_fuse = false;
+  u64 *d_bfv_dscale = nullptr;  // [L] (Q_j/q_i)^-1 R: the floor writes ModUp's scaled sources
+  u64 *d_bfv_kscale = nullptr;  // [nmod] INTT(acc) output constants: N^-1 (Q), N^-1 (P/p_k)^-1 (P), Montgomery
   std::vector<ConvTab> modup_tabs;  // host copies of d_modup (device pointers inside)
   std::vector<void *> blobs;   // device allocations owned by the context
   void *behz = nullptr;        // BEHZ device constants (BFV)
@@ -194,7 +200,9 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n);
 // INTT(acc_P) with the P limbs' key-switching inner product in its first pass
 // (ext_g != 0: ext is read as sigma_g(ext), the hoisted rotation's inner product)
-int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, u32 ext_g = 0);
+// (all_limbs: every Q u P limb with the output constants d_bfv_kscale, BFV)
+int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, u32 ext_g = 0,
+                       bool all_limbs = false);
 // (base null: sigma(c0) is not stored; the combine then reads it with base_g)
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);

@@ -313,6 +313,31 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p, u32 alpha = 0) {
       c->d_iscale = (u64 *)ctx_upload(c, isc.data(), sizeof(u64) * isc.size());
       if (!c->d_iscale) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
     }
+    // BFV relinearisation with the fused passes (bfv_ks_fused, rns.hip)
+    const u32 ndig = (L + c->alpha - 1) / c->alpha;
+    c->bfv_ks_fuse = p->scheme == FHE_SCHEME_BFV && c->log_n >= 15 && c->alpha <= 4 && c->K <= 4 && ndig <= 4;
+    if (c->bfv_ks_fuse) {
+      std::vector<u64> dsc(L), ksc(c->nmod, 0);
+      for (u32 i = 0; i < L; ++i) {
+        const u32 lo = i / c->alpha * c->alpha, hi = std::min(lo + c->alpha, L);
+        const u64 qi = c->moduli[i];
+        u64 prod = 1;
+        for (u32 m = lo; m < hi; ++m)
+          if (m != i) prod = hmul(prod, c->moduli[m] % qi, qi);
+        dsc[i] = tomont(hinv(prod, qi), qi);
+        ksc[i] = tomont(hinv((u64)c->n % qi, qi), qi);
+      }
+      for (u32 k = 0; k < c->K; ++k) {
+        const u64 pk = c->moduli[L + k];
+        u64 prod = 1;
+        for (u32 m = 0; m < c->K; ++m)
+          if (m != k) prod = hmul(prod, c->moduli[L + m] % pk, pk);
+        ksc[L + k] = tomont(hmul(hinv(prod, pk), hinv((u64)c->n % pk, pk), pk), pk);
+      }
+      c->d_bfv_dscale = (u64 *)ctx_upload(c, dsc.data(), sizeof(u64) * L);
+      c->d_bfv_kscale = (u64 *)ctx_upload(c, ksc.data(), sizeof(u64) * ksc.size());
+      if (!c->d_bfv_dscale || !c->d_bfv_kscale) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
+    }
   }
   if (p->scheme == FHE_SCHEME_BFV) {
     int rc = (p->flags & FHE_FLAG_BFV_HPS) ? hps_setup(c) : behz_setup(c);

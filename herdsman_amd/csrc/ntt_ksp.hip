@@ -64,21 +64,25 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
 // (ks_inner_kernel) formed in the first (row) pass (PRO_KSP): acc_P is never
 // stored, the P rows of acc receive INTT(acc_P) times d_iscale (ModDown's
 // source constants, as ntt_launch(..., d_iscale) gives them)
-int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, u32 ext_g) {
+int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, u32 ext_g,
+                       bool all_limbs) {
   const u32 L = c->L, K = c->K, QP = L + K;
   const size_t N = c->n;
   if (c->log_n <= 14 || ndig < 1 || ndig > 4)
     return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused P-limb inner product: log_n / digits");
+  if (all_limbs && (!c->d_bfv_kscale || c->key_pshift))
+    return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused all-limb inner product: BFV tables");
+  const u32 l0 = all_limbs ? 0 : L, nl = all_limbs ? QP : K;
   const u32 per = 65534u;  // gridDim.y, even (the polys of a ciphertext stay together)
   for (u32 p0 = 0; p0 < 2 * n; p0 += per) {
     const u32 np = std::min(per, 2 * n - p0);
     NttArgs a{};
-    a.map = LimbMap{acc + (size_t)p0 * QP * N, QP, K, L, QP, 0, 0, np};
+    a.map = LimbMap{acc + (size_t)p0 * QP * N, QP, nl, l0, QP, 0, 0, np};
     a.tw = c->d_tw_inv;
     a.mods = c->d_mods;
     a.ninv = c->d_ninv;
     a.log_n = c->log_n;
-    a.scale = c->d_iscale;
+    a.scale = all_limbs ? c->d_bfv_kscale : c->d_iscale;
     a.e_ext = ext + (size_t)(p0 / 2) * ndig * QP * N;
     a.e_ksk = ksk;
     a.e_ndig = ndig;
@@ -86,7 +90,7 @@ int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32
     a.e_kQP = ctx_key_qp(c);
     a.e_kshift = c->key_pshift;
     a.e_ext_g = ext_g & ((2u << c->log_n) - 1);
-    const u32 n_jobs = np * K;
+    const u32 n_jobs = np * nl;
     int rc;
     switch (ndig + (ext_g ? 4 : 0)) {
       case 1: rc = row_pass<PRO_KSP>(c, a, true, n_jobs); break;

@@ -280,6 +280,37 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_combine_kernel(const u64 *__restr
   out[o] = ks;
 }
 
+// Fused BFV ModDown finish (coefficient domain, bfv_ks_fused): the P -> Q
+// conversion of acc's P limbs (already scaled by INTT(acc)'s output constants
+// d_bfv_kscale, so they are the conversion's v_k) as 31-bit column sums, and the
+// combine, per element:  out_b[i] = base_b[i] + (acc_b[i] - sum_k v_k [P/p_k]_{q_i}) P^-1.
+// h = the ModDown table [K][L] ((P/p_k) R mod q_i), K <= 4.
+template <bool SP>
+__global__ void __launch_bounds__(EW_BLOCK) bfv_moddown_kernel(const u64 *__restrict__ acc, const u64 *base, u64 *out,
+                                                               const u64 *__restrict__ h, const u64 *pinv,
+                                                               const ModInfo *mods, u32 L, u32 K, u32 QP,
+                                                               u32 log_n, u32 add_mask) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 p = blockIdx.y / L, i = blockIdx.y % L;  // p = 2 ct + b
+  const size_t N = (size_t)1 << log_n;
+  const ModInfo m = mods[i];
+  const u64 *ap = acc + (size_t)p * QP * N + k;
+  u64 v[4];
+  u32 h0[4], h1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool on = j < (int)K;
+    v[j] = on ? ap[(size_t)(L + j) * N] : 0;
+    if (on) split31(h[(size_t)j * L + i], h0[j], h1[j]);
+    else h0[j] = h1[j] = 0;
+  }
+  const u64 cv = csub63(dot_cols<4, SP>(v, h0, h1, m), m.q);
+  u64 ks = csub63(mont_mul<SP>(sub_mod(ap[(size_t)i * N], cv, m.q), pinv[i], m), m.q);
+  const size_t o = ((size_t)p * L + i) * N + k;
+  if (add_mask & (1u << (p & 1))) ks = add_mod(ks, base[o], m.q);
+  out[o] = ks;
+}
+
 // Rotation input: (c0, c1) -> sigma_g, fused with the key-switch preparation:
 //   base[ct][0] = sigma(c0); dc[ct] = sigma(c1); ext[ct][own] = sigma(c1) * R.
 // NTT domain (CKKS): slot permutation; coefficient domain (BFV): signed gather.
@@ -406,7 +437,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
                                                               u64 *__restrict__ out01, u64 *__restrict__ dc,
                                                               u64 *__restrict__ ext, const BehzDev *bz,
                                                               const ModInfo *mods, u32 log_n, u32 QP, u32 dig_len,
-                                                              u32 ndig) {
+                                                              u32 ndig, const u64 *dsc) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 ct = blockIdx.y / 3, p = blockIdx.y % 3;
   const size_t N = (size_t)1 << log_n;
@@ -450,7 +481,8 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
     const u64 cq = behz_dot<NL, SP>(w, &bz->h_b_q_R[0][i], BEHZ_MAXL, nB - 1, m);
     const u64 ab = csub63(mont_mul<SP>(amag, bz->b_mod_q_R[i], m), m.q);
     const u64 r = csub63(cq + (neg ? ab : m.q - ab), m.q);  // cq -/+ ab (ab = 0 gives cq + q -> cq)
-    o[i * N] = r;
+    // dsc (fused BFV relinearisation): dc holds ModUp's scaled sources r (Q_j/q_i)^-1
+    o[i * N] = p == 2 && dsc ? csub63(mont_mul<SP>(r, dsc[i], m), m.q) : r;
     if (p == 2) ext[((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k] = csub63(mont_mul<SP>(r, m.r2, m), m.q);
   }
 }
@@ -542,7 +574,7 @@ __global__ void __launch_bounds__(EW_BLOCK) hps_scale_kernel(const u64 *__restri
                                                              u64 *__restrict__ out01, u64 *__restrict__ dc,
                                                              u64 *__restrict__ ext, const HpsDev *hp,
                                                              const ModInfo *mods, u32 log_n, u32 QP, u32 dig_len,
-                                                             u32 ndig) {
+                                                             u32 ndig, const u64 *dsc) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 ct = blockIdx.y / 3, p = blockIdx.y % 3;
   const size_t N = (size_t)1 << log_n;
@@ -579,7 +611,7 @@ __global__ void __launch_bounds__(EW_BLOCK) hps_scale_kernel(const u64 *__restri
     const u64 cq = dot_mont<NL + 1, SP>(y, &hp->pstar_R[0][i], BEHZ_MAXL, nB, m);
     const u64 vp = csub63(mont_mul<SP>(v, hp->P_R[i], m), m.q);
     const u64 res = sub_mod(cq, vp, m.q);
-    o[i * N] = res;
+    o[i * N] = p == 2 && dsc ? csub63(mont_mul<SP>(res, dsc[i], m), m.q) : res;
     if (p == 2) ext[((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k] = csub63(mont_mul<SP>(res, m.r2, m), m.q);
   }
 }
@@ -699,14 +731,15 @@ int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
 }
 
 template <bool SP>
-int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *dc, u64 *ext, u32 n, u32 ndig,
+                    const u64 *dsc) {
   dim3 grid(c->n / EW_BLOCK, n * 3);
   const BehzDev *bz = (const BehzDev *)c->behz;
   const u32 QP = c->L + c->K;
-  if (c->L == 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
-  else if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
-  else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
-  else hipLaunchKernelGGL((behz_floor_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  if (c->L == 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else hipLaunchKernelGGL((behz_floor_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
   return fhe_check(c, hipGetLastError(), "behz_floor");
 }
 
@@ -722,14 +755,15 @@ int hps_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
 }
 
 template <bool SP>
-int hps_scale_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+int hps_scale_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *dc, u64 *ext, u32 n, u32 ndig,
+                   const u64 *dsc) {
   dim3 grid(c->n / EW_BLOCK, n * 3);
   const HpsDev *hp = (const HpsDev *)c->hps;
   const u32 QP = c->L + c->K;
-  if (c->L == 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig);
-  else if (c->L <= 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig);
-  else if (c->L <= 16) hipLaunchKernelGGL((hps_scale_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig);
-  else hipLaunchKernelGGL((hps_scale_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig);
+  if (c->L == 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else if (c->L <= 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else if (c->L <= 16) hipLaunchKernelGGL((hps_scale_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else hipLaunchKernelGGL((hps_scale_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
   return fhe_check(c, hipGetLastError(), "hps_scale");
 }
 
@@ -791,6 +825,9 @@ struct KsWs {
   u64 *dc, *ext, *acc, *conv;
   u32 ndig;
 };
+#ifndef BFV_KS_FUSE
+#define BFV_KS_FUSE 1  // BFV mul+relin: the fused relinearisation (bfv_ks_fused) where the context allows it
+#endif
 #ifndef KSP_FUSE
 #define KSP_FUSE 1  // the P limbs' inner product inside INTT(acc_P)'s first pass (0: ks_inner_kernel)
 #endif
@@ -1180,6 +1217,46 @@ int hps_setup(fhe_ctx *c) {
   return c->hps ? FHE_OK : FHE_ERR_OOM;
 }
 
+template <bool SP>
+static int bfv_moddown_impl(fhe_ctx *c, const u64 *acc, const u64 *base, u64 *out, u32 n, u32 add_mask) {
+  const u32 L = c->L, per = std::max<u32>(1, kMaxGridY / L);
+  const size_t N = c->n, QP = c->L + c->K;
+  for (u32 p0 = 0; p0 < 2 * n; p0 += per) {
+    const u32 np = std::min(per, 2 * n - p0);
+    hipLaunchKernelGGL((bfv_moddown_kernel<SP>), dim3(c->n / EW_BLOCK, np * L), dim3(EW_BLOCK), 0, c->stream,
+                       acc + (size_t)p0 * QP * N, base + (size_t)p0 * L * N, out + (size_t)p0 * L * N, c->moddown.h,
+                       c->d_pinv, c->d_mods, L, c->K, (u32)QP, c->log_n, add_mask);
+    int rc = fhe_check(c, hipGetLastError(), "bfv_moddown_kernel");
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
+// BFV relinearisation at two-pass sizes (c->bfv_ks_fuse), the coefficient-
+// domain counterpart of keyswitch_run's fused CKKS path, on a prepared scratch
+// whose dc holds ModUp's SCALED sources (the floor's dsc) and whose ext holds
+// the own-digit limbs d R (coefficient form):
+//   ModUp of digit j inside the column pass of the NTT of its converted limbs
+//   (ntt_fwd_modup_launch), the own limbs' NTT, then INTT(acc) over every limb
+//   of Q u P with the inner product in its first pass (PRO_KSP over all
+//   limbs; the P limbs come out as ModDown's v_k, the Q limbs as plain
+//   coefficients), and ModDown + combine in one kernel (bfv_moddown_kernel):
+//   no ModUp, inner-product or conversion intermediate reaches HBM.
+static int bfv_ks_fused(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask) {
+  const u32 L = c->L, QP = L + c->K, N = c->n, ndig = w.ndig;
+  int rc;
+  for (u32 j = 0; j < ndig; ++j)
+    if ((rc = ntt_fwd_modup_launch(c, w.dc, w.ext, n, ndig, j))) return rc;
+  for (u32 j = 0; j < ndig; ++j) {
+    const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
+    if ((rc = ntt_launch(c, LimbMap{w.ext + (size_t)j * QP * N, ndig * QP, hi - lo, lo, hi - lo, 0, 0, n}, false,
+                         false, c->special)))
+      return rc;
+  }
+  if ((rc = ntt_inv_ksp_launch(c, w.acc, w.ext, ksk, n, ndig, 0, true))) return rc;
+  return SP_DISPATCH(c, bfv_moddown_impl, c, w.acc, base, out, n, add_mask);
+}
+
 size_t bfv_mul_ws_bytes(const fhe_ctx *c, u32 n) {
   const size_t N = c->n, L = c->L, nB = c->nB;
   return sizeof(u64) * N * n * (4 * L + 4 * nB + 3 * L + 3 * nB) + keyswitch_ws_bytes(c, n);
@@ -1212,9 +1289,11 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   if ((rc = ntt_inv_bfv_tensor_launch(c, xb, xb + (size_t)n * 2 * nB * N, eb, nB, bsk0, n))) return rc;
   // 5. scale and round: r0, r1 -> out; r2 -> the key-switch scratch, prepared
   //    (BEHZ floor, or HPS simple scaling + exact P -> Q)
-  if ((rc = c->hps ? SP_DISPATCH(c, hps_scale_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig)
-                   : SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig)))
+  const u64 *dsc = c->bfv_ks_fuse && BFV_KS_FUSE ? c->d_bfv_dscale : nullptr;
+  if ((rc = c->hps ? SP_DISPATCH(c, hps_scale_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig, dsc)
+                   : SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig, dsc)))
     return rc;
   // 6. relinearize r2 and add to (r0, r1)
+  if (dsc) return bfv_ks_fused(c, w, rlk, out, out, n, 3u);
   return keyswitch_run(c, w, rlk, out, out, n, 3u, false);
 }
