@@ -852,7 +852,7 @@ static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
 // the converted limbs, into w.ext) runs once per input, ks_finish (steps 4-6:
 // inner product, ModDown) once per key.
 static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is_coef) {
-  const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
+  const u32 L = c->L, QP = L + c->K, N = c->n, ndig = w.ndig;
   u64 *dc = w.dc, *ext = w.ext;
   int rc;
   // CKKS at two-pass sizes: ModUp runs inside the column pass of the NTT of
@@ -879,7 +879,6 @@ static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is
     // (< 8q) NTT outputs as they are, so the last pass skips canonicalising
     if ((rc = ntt_launch(c, m, false, false, c->special))) return rc;
   }
-  (void)K;
   return FHE_OK;
 }
 
