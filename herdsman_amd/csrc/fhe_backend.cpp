@@ -712,6 +712,9 @@ int fhe_rotate_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uin
     // the combine reads c0 through sigma_g: outs must not overlap ct
     if (n_ct && outs[r] < ct + n_ct * cw && ct < outs[r] + n_ct * cw)
       return fhe_fail(c, FHE_ERR_INVALID, "hoisted rotation output overlaps its input");
+    for (uint32_t q = 0; q < r && n_ct; ++q)
+      if (outs[r] < outs[q] + n_ct * cw && outs[q] < outs[r] + n_ct * cw)
+        return fhe_fail(c, FHE_ERR_INVALID, "hoisted rotation outputs overlap each other");
   }
   if (!n_ct || !n_rot) return FHE_OK;
   std::vector<u64 *> o(n_rot);

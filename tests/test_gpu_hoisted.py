@@ -116,6 +116,11 @@ def test_hoisted_errors(hb, metric):
     assert lib.fhe_rotate_hoisted(c.h, hb._ptr(ct), 1, C.addressof(ga), C.addressof(ka), C.addressof(oa), 1) \
         == hb.FHE_ERR_INVALID
     assert lib.fhe_rotate_hoisted(c.h, hb._ptr(ct), 0, None, None, None, 1) == hb.FHE_OK
+    ga2 = (C.c_uint32 * 2)(o.galois_elt(1), o.galois_elt(2))
+    ka2 = (C.c_uint64 * 2)(hb._ptr(k), hb._ptr(k))
+    oa2 = (C.c_uint64 * 2)(hb._ptr(out), hb._ptr(out))  # two outputs on one buffer
+    assert lib.fhe_rotate_hoisted(c.h, hb._ptr(ct), 2, C.addressof(ga2), C.addressof(ka2), C.addressof(oa2), 1) \
+        == hb.FHE_ERR_INVALID
     bfv = hb.Context(SCHEME_BFV, 12, 3, 1, 1, t=65537)
     z = hb.empty((1, 2, 3, bfv.n))
     kz = hb.empty(bfv.key_shape())
