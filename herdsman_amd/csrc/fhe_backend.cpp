@@ -497,7 +497,7 @@ int fhe_reserve(fhe_ctx *c, uint32_t max_batch) {
   max_batch = std::min(max_batch, kCtChunk);  // ops run in passes of at most kCtChunk ciphertexts
   size_t need = (size_t)sizeof(u64) * c->n * max_batch * 2 * c->L;  // rotate / mul scratch
   if (c->K) need += keyswitch_ws_bytes(c, max_batch);
-  if (c->K && c->params.scheme == FHE_SCHEME_CKKS) need = std::max(need, rotate_hoisted_ws_bytes(c, max_batch));
+  if (c->K) need = std::max(need, rotate_hoisted_ws_bytes(c, max_batch));
   if (c->nB) need = std::max(need, bfv_mul_ws_bytes(c, max_batch));
   void *p;
   return ctx_workspace(c, need, &p);
@@ -700,7 +700,6 @@ int fhe_rotate(fhe_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, u
 int fhe_rotate_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                        const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct) {
   if (!c) return FHE_ERR_INVALID;
-  if (c->params.scheme != FHE_SCHEME_CKKS) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "hoisted rotations are CKKS only");
   if (c->K == 0) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "context has no special primes (K = 0)");
   if (n_rot && (!galois || !gks || !outs)) return fhe_fail(c, FHE_ERR_INVALID, "null array");
   DeviceBind bind(c);

@@ -694,6 +694,13 @@ int ks_prep_impl(fhe_ctx *c, const u64 *d, u32 d_stride, u64 *dc, u64 *ext, u32 
   return fhe_check(c, hipGetLastError(), "ks_prep_kernel");
 }
 
+// g^-1 mod 2N (g odd) by Newton iteration on the 2-adic inverse
+static u32 galois_inv(u32 g, u32 log_n) {
+  u32 inv = g;
+  for (int i = 0; i < 5; ++i) inv *= 2u - g * inv;
+  return inv & ((2u << log_n) - 1);
+}
+
 template <bool SP>
 int automorph_ks_impl(fhe_ctx *c, const u64 *ct, u64 *base, u64 *dc, u64 *ext, u32 g, u32 n, u32 ndig, bool ntt) {
   dim3 grid(c->n / EW_BLOCK, n * c->L);
@@ -702,9 +709,7 @@ int automorph_ks_impl(fhe_ctx *c, const u64 *ct, u64 *base, u64 *dc, u64 *ext, u
     hipLaunchKernelGGL((automorph_ks_kernel<SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, ct, base, dc, ext, g,
                        c->d_mods, c->L, QP, c->alpha, ndig, c->log_n);
   } else {
-    u32 inv = g;  // g^-1 mod 2N (g odd) by Newton iteration on the 2-adic inverse
-    for (int i = 0; i < 5; ++i) inv *= 2u - g * inv;
-    inv &= (2u * c->n) - 1;
+    const u32 inv = galois_inv(g, c->log_n);
     hipLaunchKernelGGL((automorph_ks_kernel<SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, ct, base, dc, ext, inv,
                        c->d_mods, c->L, QP, c->alpha, ndig, c->log_n);
   }
@@ -989,13 +994,40 @@ __global__ void __launch_bounds__(EW_BLOCK) aut_rows_kernel(const u64 *__restric
   const u32 sk = __brev((e2 - 1) >> 1) >> (32 - log_n);
   dst[(grp * dst_gs + i) * N + k] = src[(grp * src_gs + i) * N + sk];
 }
-static int aut_rows(fhe_ctx *c, const u64 *src, u32 src_gs, u64 *dst, u32 dst_gs, u32 rpg, u32 n_rows, u32 g) {
+// the coefficient-domain automorphism of whole rows (BFV): dst[k g mod 2N] =
+// +-src[k], i.e. dst[j] = +-src[j g^-1 mod 2N] (automorph_ks_kernel's map);
+// row r of a group is limb r % rpg (its modulus for the sign flip)
+__global__ void __launch_bounds__(EW_BLOCK) aut_rows_coef_kernel(const u64 *__restrict__ src, u32 src_gs,
+                                                                 u64 *__restrict__ dst, u32 dst_gs, u32 rpg,
+                                                                 u32 ginv, const ModInfo *mods, u32 log_n) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x, r = blockIdx.y;
+  const size_t N = (size_t)1 << log_n, grp = r / rpg, i = r % rpg;
+  const u32 n = 1u << log_n, j0 = (u32)(((u64)k * ginv) & (2 * n - 1));
+  const u64 *s = src + (grp * src_gs + i) * N;
+  u64 v;
+  if (j0 < n) {
+    v = s[j0];
+  } else {
+    const u64 x = s[j0 - n];
+    v = x ? mods[i].q - x : 0;
+  }
+  dst[(grp * dst_gs + i) * N + k] = v;
+}
+
+static int aut_rows(fhe_ctx *c, const u64 *src, u32 src_gs, u64 *dst, u32 dst_gs, u32 rpg, u32 n_rows, u32 g,
+                    bool coef = false) {
   const u32 per = kMaxGridY / rpg * rpg;
   const size_t N = c->n;
   for (u32 r0 = 0; r0 < n_rows; r0 += per) {
     const u32 nr = std::min(per, n_rows - r0), g0 = r0 / rpg;
-    hipLaunchKernelGGL(aut_rows_kernel, dim3(c->n / EW_BLOCK, nr), dim3(EW_BLOCK), 0, c->stream,
-                       src + (size_t)g0 * src_gs * N, src_gs, dst + (size_t)g0 * dst_gs * N, dst_gs, rpg, g, c->log_n);
+    if (coef)
+      hipLaunchKernelGGL(aut_rows_coef_kernel, dim3(c->n / EW_BLOCK, nr), dim3(EW_BLOCK), 0, c->stream,
+                         src + (size_t)g0 * src_gs * N, src_gs, dst + (size_t)g0 * dst_gs * N, dst_gs, rpg, g,
+                         c->d_mods, c->log_n);
+    else
+      hipLaunchKernelGGL(aut_rows_kernel, dim3(c->n / EW_BLOCK, nr), dim3(EW_BLOCK), 0, c->stream,
+                         src + (size_t)g0 * src_gs * N, src_gs, dst + (size_t)g0 * dst_gs * N, dst_gs, rpg, g,
+                         c->log_n);
     int rc = fhe_check(c, hipGetLastError(), "aut_rows_kernel");
     if (rc) return rc;
   }
@@ -1005,14 +1037,15 @@ static int aut_rows(fhe_ctx *c, const u64 *src, u32 src_gs, u64 *dst, u32 dst_gs
 // the gather path (sigma_g inside the fused inner-product passes) needs only
 // the key-switch scratch; the generic one also sigma_g(ext) and sigma_g(c0)
 static bool hoisted_gather(const fhe_ctx *c) {
-  return c->log_n > 14 && ks_fused_inner(c, (c->L + c->alpha - 1) / c->alpha, true);
+  return c->params.scheme == FHE_SCHEME_CKKS && c->log_n > 14 &&
+         ks_fused_inner(c, (c->L + c->alpha - 1) / c->alpha, true);
 }
 size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n) {
   const size_t N = c->n, L = c->L, QP = c->L + c->K, ndig = (c->L + c->alpha - 1) / c->alpha;
   return keyswitch_ws_bytes(c, n) + (hoisted_gather(c) ? 0 : sizeof(u64) * N * n * (ndig * QP + 2 * L));
 }
 
-// Hoisted rotations (CKKS; oracle orc_rotate_hoisted, OpenFHE EvalFastRotation):
+// Hoisted rotations (oracle orc_rotate_hoisted, OpenFHE EvalFastRotation):
 // c1 is extended ONCE (INTT, ModUp, NTT of the converted limbs), then every
 // Galois element g_r key-switches sigma_g(ext) -- not ModUp(sigma_g(c1)), so the
 // bits differ from rotate_impl's by the ModUp error term -- and adds sigma_g(c0).
@@ -1020,7 +1053,9 @@ size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n) {
 // inner-product passes (EPI_KSQG / PRO_KSPG) and the combine reads c0 through
 // sigma_g, so a rotation costs its key switch's inner product and ModDown only.
 // Otherwise sigma_g(ext) and sigma_g(c0) are materialised (aut_rows_kernel).
-// outs[r] must not overlap ct.
+// BFV (coefficient form) takes that path too: ext is permuted in the NTT
+// domain the inner product runs in, c0 by the signed coefficient map, and the
+// finish is the coefficient-domain ModDown.  outs[r] must not overlap ct.
 int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois, const u64 *const *gks,
                         u64 *const *outs, u32 n) {
   const size_t LN = (size_t)c->L * c->n, QP = c->L + c->K;
@@ -1030,23 +1065,24 @@ int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois,
   const KsWs w = ks_layout(c, n, (u64 *)ws);
   u64 *ext_g = w.conv + n * 2 * LN;      // [n][ndig][QP][N] (generic path)
   u64 *base = ext_g + n * w.ndig * QP * c->n;  // [n][2][L][N], poly 0 = sigma(c0) (generic path)
-  const bool gather = hoisted_gather(c);
-  if (c->log_n > 14) {
+  const bool gather = hoisted_gather(c), ckks = c->params.scheme == FHE_SCHEME_CKKS;
+  if (ckks && c->log_n > 14) {
     // the identity automorphism: INTT(c1) with the ModUp source scaling and
     // the own-digit slots c1 R, as rotate_impl's fused prologue
     if ((rc = ntt_inv_automorph_launch(c, ct, 1u, nullptr, w.dc, w.ext, n, w.ndig))) return rc;
   } else if ((rc = SP_DISPATCH(c, ks_prep_impl, c, ct + LN, 2 * c->L, w.dc, w.ext, n, w.ndig))) {
     return rc;
   }
-  if ((rc = ks_extend(c, w, n, true, c->log_n > 14))) return rc;
+  if ((rc = ks_extend(c, w, n, ckks, ckks && c->log_n > 14))) return rc;
   for (u32 r = 0; r < n_rot; ++r) {
     const u32 g = galois[r];
     if (gather) {
       rc = ks_finish(c, w, w.ext, gks[r], ct, outs[r], n, 1u, true, g, g);
     } else {
       if ((rc = aut_rows(c, w.ext, w.ndig * QP, ext_g, w.ndig * QP, w.ndig * QP, n * w.ndig * QP, g))) return rc;
-      if ((rc = aut_rows(c, ct, 2 * c->L, base, 2 * c->L, c->L, n * c->L, g))) return rc;
-      rc = ks_finish(c, w, ext_g, gks[r], base, outs[r], n, 1u, true, 0, 0);
+      const u32 gb = ckks ? g : galois_inv(g, c->log_n);
+      if ((rc = aut_rows(c, ct, 2 * c->L, base, 2 * c->L, c->L, n * c->L, gb, !ckks))) return rc;
+      rc = ks_finish(c, w, ext_g, gks[r], base, outs[r], n, 1u, ckks, 0, 0);
     }
     if (rc) return rc;
   }

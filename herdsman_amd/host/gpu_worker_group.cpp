@@ -848,7 +848,6 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
         // sum of hoisted rotations: one fhe_rotate_hoisted_at over every step
         // in the mask, then the adds (bit 0 adds the input itself)
         if (stack.empty()) throw std::runtime_error("circuit stack underflow");
-        if (s.scheme != FHE_SCHEME_CKKS) throw std::runtime_error("rotsum is CKKS only");
         const uint32_t mask = (uint32_t)ins.arg;
         if (mask == 0 || (mask >> 31)) throw std::runtime_error("rotsum step mask must be in [1, 2^31)");
         const uint32_t m = stack.back().level;

@@ -55,7 +55,7 @@ struct CryptoKeyPtr {
 // Stand-in circuit: a stack program over the ciphertexts of one row.
 // CKKS operands may sit at different levels: binary ops run at the lower one
 // (the other operand's extra limbs dropped), RESCALE drops one level.
-// ROTSUM (CKKS) replaces the top with sum_{i in arg} rot_i(top), arg a bit mask
+// ROTSUM replaces the top with sum_{i in arg} rot_i(top), arg a bit mask
 // of step counts 0..30 (bit 0: the ciphertext itself), the rotations hoisted
 // (one ModUp of c1 for all of them: a baby-step block of a linear transform).
 enum class CtOp : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4, RESCALE = 5, ROTSUM = 6 };

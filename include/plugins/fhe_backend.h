@@ -142,7 +142,7 @@ int fhe_keyswitch(fhe_ctx *ctx, const uint64_t *d, const uint64_t *ksk, uint64_t
 /* automorphism X -> X^galois_elt followed by key switching with the Galois key */
 int fhe_rotate(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const uint64_t *gk, uint64_t *out,
                uint32_t n_ct);
-/* hoisted rotations (CKKS): n_rot Galois elements applied to the same n_ct
+/* hoisted rotations (CKKS and BFV): n_rot Galois elements applied to the same n_ct
  * ciphertexts, c1's ModUp computed once (OpenFHE EvalFastRotationPrecompute +
  * EvalFastRotation, which herdsman's linked library provides for rotation-heavy
  * circuits).  galois_elts, gks, outs: HOST arrays of n_rot entries; gks[r] is a

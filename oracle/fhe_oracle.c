@@ -858,10 +858,12 @@ void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t
   rotate_lvl(c, ct, g, gk, out, n_ct, c->L);
 }
 
-/* Hoisted rotations (CKKS): for each Galois element g_r of galois[0..n_rot),
+/* Hoisted rotations: for each Galois element g_r of galois[0..n_rot),
  * outs[r] = (sigma(c0) + KS0, KS1) with KS over sigma_g(ModUp(c1)) and key
  * gks[r] -- one ModUp of c1 serves every rotation.  gks [n_rot][key],
- * outs [n_rot][n_ct][2][L][N]. */
+ * outs [n_rot][n_ct][2][L][N].  CKKS: NTT form; BFV: coefficient form (the
+ * extension is permuted in the NTT domain the key-switch inner product runs
+ * in, c0 by the signed coefficient map; OpenFHE EvalFastRotation serves both). */
 static void rotate_hoisted_lvl(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                                const uint64_t *gks, uint64_t *outs, uint32_t n_ct, uint32_t lvl) {
   const size_t L = lvl, N = c->n, CT = 2 * L * N, KW = (size_t)c->dnum * 2 * (c->L + c->K) * N;
@@ -870,8 +872,10 @@ static void rotate_hoisted_lvl(const orc_ctx *c, const uint64_t *ct, uint32_t n_
     for (long i = 0; i < (long)n_ct; ++i) {
       uint64_t *o = outs + ((size_t)r * n_ct + i) * CT;
       uint64_t *ks = malloc(sizeof(uint64_t) * CT);
-      keyswitch_lvl_g(c, ct + i * CT + L * N, gks + r * KW, ks, 1, (uint32_t)L, galois[r]);
-      orc_automorph_ntt(c, ct + i * CT, o, galois[r], 1, (uint32_t)L);
+      const int ckks = c->scheme == ORC_SCHEME_CKKS;
+      keyswitch_lvl_g(c, ct + i * CT + L * N, gks + r * KW, ks, ckks, (uint32_t)L, galois[r]);
+      if (ckks) orc_automorph_ntt(c, ct + i * CT, o, galois[r], 1, (uint32_t)L);
+      else orc_automorph_coef(c, ct + i * CT, o, galois[r], 1, 0, (uint32_t)L);
       orc_add(c, o, ks, o, 1, 0, (uint32_t)L);
       memcpy(o + L * N, ks + L * N, sizeof(uint64_t) * L * N);
       free(ks);

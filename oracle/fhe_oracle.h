@@ -91,7 +91,7 @@ void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t galois, const uin
                 uint64_t *out, uint32_t n_ct);
 uint32_t orc_galois_elt(const orc_ctx *c, int32_t steps);
 
-/* hoisted rotations of ct [n_ct][2][L][N] (CKKS): outs [n_rot][n_ct][2][L][N],
+/* hoisted rotations of ct [n_ct][2][L][N] (CKKS in NTT form, BFV in coefficient form): outs [n_rot][n_ct][2][L][N],
  * gks [n_rot][dnum][2][L+K][N]; KS over sigma_g(ModUp(c1)) (one ModUp for all) */
 void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                         const uint64_t *gks, uint64_t *outs, uint32_t n_ct);

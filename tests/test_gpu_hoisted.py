@@ -127,8 +127,22 @@ def test_hoisted_errors(hb, metric):
     ka[0] = hb._ptr(kz)
     oa[0] = hb._ptr(hb.empty((1, 2, 3, bfv.n)))
     ga[0] = 5
-    assert lib.fhe_rotate_hoisted(bfv.h, hb._ptr(z), 1, C.addressof(ga), C.addressof(ka), C.addressof(oa), 1) \
-        == hb.FHE_ERR_UNSUPPORTED
+    # BFV has no reduced levels
+    assert lib.fhe_rotate_hoisted_at(bfv.h, hb._ptr(z), 1, C.addressof(ga), C.addressof(ka), C.addressof(oa), 1,
+                                     2) == hb.FHE_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("log_n,L,K,dnum", [(15, 8, 4, 2), (12, 5, 2, 3)])
+def test_bfv_hoisted(hb, log_n, L, K, dnum):
+    """BFV (coefficient form): ext permuted in the NTT domain, c0 by the signed
+    coefficient map, the coefficient-domain ModDown; C3 parameters and a
+    one-pass size with a partial digit."""
+    o = Oracle(SCHEME_BFV, log_n, L, K, dnum, t=65537)
+    c = hb.Context(SCHEME_BFV, log_n, L, K, dnum, t=65537, moduli=o.moduli)
+    ct = o.uniform((2, 2, L, o.n), seed=1500 + log_n)
+    gs = [o.galois_elt(1), o.galois_elt(-4), 2 * o.n - 1]
+    gks = [o.uniform(o.key_shape(), seed=1510 + i) for i in range(len(gs))]
+    assert np.array_equal(_run(hb, c, ct, gs, gks), o.rotate_hoisted(ct, gs, np.stack(gks)))
 
 
 def test_hoisted_chunked_batch(hb):

@@ -139,3 +139,36 @@ def test_ckks_hoisted_rotations_at_level_decrypt():
         dec = crt_centered(o.ntt_inv(m[None])[0], Q)
         want = [delta * v for v in automorph_int(u, g)]
         assert max(abs(a - b) for a, b in zip(dec, want)) < 2 ** 30
+
+
+@pytest.mark.parametrize("mult", ["behz", "hps"])
+def test_bfv_hoisted_rotations_decrypt_exactly(mult):
+    """BFV hoisted rotations (coefficient-form ciphertexts; the extension of c1
+    permuted in the NTT domain of the inner product, c0 by the signed
+    coefficient map) decrypt exactly to the rotated message, also after a
+    product."""
+    t = 65537
+    o = Oracle(SCHEME_BFV, 10, 4, 2, 2, t=t, bfv_mult=mult)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    Qp = math.prod(Q)
+    s, s_qp = _keys(o)
+    rng = random.Random(11)
+    delta = Qp // t
+    m1 = [rng.randrange(t) for _ in range(o.n)]
+    m2 = [rng.randrange(t) for _ in range(o.n)]
+    c1 = o.encrypt(to_rns([delta * x for x in m1], Q), s_qp, 606)
+    c2 = o.encrypt(to_rns([delta * x for x in m2], Q), s_qp, 707)
+    rlk = o.switch_key(_square_ntt(o, s_qp), s_qp, seed=12)
+    prod = o.mul_relin(c1[None], c2[None], rlk)[0]
+    want_prod = [v % t for v in negacyclic_int(m1, m2)]
+
+    def dec(ct):
+        v = crt_centered(o.decrypt(ct, s_qp), Q)
+        return [((t * x + Qp // 2) // Qp) % t for x in v]
+
+    gs = [o.galois_elt(k) for k in (1, -2, 5)]
+    gks = np.stack([o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=50 + i) for i, g in enumerate(gs)])
+    outs = o.rotate_hoisted(np.stack([c1, prod]), gs, gks)
+    for r, g in enumerate(gs):
+        assert dec(outs[r, 0]) == [v % t for v in automorph_int(m1, g)]
+        assert dec(outs[r, 1]) == [v % t for v in automorph_int(want_prod, g)]

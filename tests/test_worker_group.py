@@ -198,6 +198,29 @@ def test_gpu_map_task_rotsum_hoisted(wg_run, tmp_path, log_n, steps, lvl):
 
 
 @pytest.mark.gpu
+def test_gpu_map_task_rotsum_bfv(wg_run, tmp_path):
+    """ROTSUM on BFV rows (C3 parameters): hoisted rotations in coefficient form."""
+    from oracle_ffi import SCHEME_BFV
+    o, storage, keys = _setup(tmp_path, SCHEME_BFV, 15, 8, 4, 2, t=65537)
+    rows = 2
+    a = o.uniform((rows, 2, o.L, o.n), seed=81)
+    rlk = o.uniform(o.key_shape(), seed=82)
+    steps = (0, 2, 5)
+    gs = [o.galois_elt(k) for k in steps if k]
+    gks = [o.uniform(o.key_shape(), seed=83 + i) for i in range(len(gs))]
+    write_partition(os.path.join(storage, "sb", "fa", "1"), [ct_row(o, [a[i]]) for i in range(rows)])
+    write_keys(os.path.join(keys, "sb", "1.key"), o, rlk, dict(zip(gs, gks)))
+    r = subprocess.run([wg_run, "map", storage, keys, "sb", "1", params_arg(o, str(tmp_path)), "fa", "1", "fb",
+                        "in0", "rotsum:0,2,5"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.stack([parse_row(o, p) for p in read_partition(os.path.join(storage, "sb", "fb", "1"))])
+    terms = list(o.rotate_hoisted(a, gs, np.stack(gks))) + [a]
+    qs = o.moduli[:o.L].astype(object)[None, None, :, None]
+    want = sum(t.astype(object) for t in terms) % qs
+    assert np.array_equal(got, want.astype(np.uint64))
+
+
+@pytest.mark.gpu
 def test_gpu_map_task_ckks_levels(wg_run, tmp_path):
     """A depth-2 CKKS circuit through the worker group: rows carry ciphertexts at
     levels 12, 12 and 11; in0 in1 mul rescale in1 mul in2 add rescale runs the
