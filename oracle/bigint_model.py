@@ -336,12 +336,18 @@ def rotate(p: Params, ct, g: int, gk):
 
 
 def rotate_hoisted(p: Params, ct, gs, gks):
-    """CKKS rotations of one ciphertext by every g in gs sharing one ModUp of
-    c1: KS over sigma_g(ModUp(c1)) with key gks[r] (OpenFHE EvalFastRotation)."""
+    """Rotations of one ciphertext by every g in gs sharing one ModUp of c1: KS
+    over sigma_g(ModUp(c1)) with key gks[r] (OpenFHE EvalFastRotation).  CKKS in
+    the NTT domain; BFV in the coefficient domain (c0 by the signed coefficient
+    map, the extension permuted in the NTT domain of the inner product)."""
+    ckks = p.scheme == "ckks"
     out = []
     for g, gk in zip(gs, gks):
-        c0 = [automorph_ntt(x, g) for x in ct[0]]
-        ks0, ks1 = keyswitch(p, ct[1], gk, True, None, g)
+        if ckks:
+            c0 = [automorph_ntt(x, g) for x in ct[0]]
+        else:
+            c0 = [automorph_coef(x, g, p.moduli[i]) for i, x in enumerate(ct[0])]
+        ks0, ks1 = keyswitch(p, ct[1], gk, ckks, None, g)
         out.append([[[(x + y) % p.moduli[i] for x, y in zip(c0[i], ks0[i])] for i in range(p.L)], ks1])
     return out
 

@@ -102,6 +102,24 @@ def gen_bfv(rng):
              out_mul=arr(out_mul), out_add=arr(out_add), g=np.uint32(g), out_rot=arr(out_rot))
 
 
+def gen_bfv_hoisted(rng):
+    """Hoisted BFV rotations (coefficient form) for steps 1, -3 and the
+    conjugation-like element 2N - 1, each with its own key."""
+    log_n, L, K, dnum, t = 10, 4, 2, 2, 65537
+    n = 1 << log_n
+    Q = M.gen_primes(60, log_n, L)
+    P = M.gen_primes(61, log_n, K, exclude=Q)
+    Bsk = M.gen_primes(61, log_n, L + 1, exclude=Q + P)
+    p = M.Params(log_n, L, K, dnum, Q + P + Bsk, "bfv", t)
+    ct = [rand_limbs(rng, Q, n) for _ in range(2)]
+    gs = [M.galois_elt(log_n, 1), M.galois_elt(log_n, -3), 2 * n - 1]
+    gks = [[[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(dnum)] for _ in gs]
+    out = M.rotate_hoisted(p, ct, gs, gks)
+    np.savez(os.path.join(HERE, "bfv_hoisted_n1024_l4.npz"), log_n=np.uint32(log_n), L=np.uint32(L),
+             K=np.uint32(K), dnum=np.uint32(dnum), t=np.uint64(t), moduli=arr(Q + P + Bsk), ct=arr(ct),
+             galois=np.array(gs, dtype=np.uint32), gks=arr(gks), out=arr(out))
+
+
 def gen_bfv_hps(rng):
     """BFV mul+relin by HPS (oracle/bigint_model.py bfv_mul_relin_hps, which also
     checks each scaled tensor output against round(t d / Q) on integers)."""
@@ -177,6 +195,7 @@ def main():
     gen_ckks_levels(random.Random(0x4C564C53))
     gen_bfv_hps(random.Random(0x485053))
     gen_ckks_hoisted(random.Random(0x484F4953))
+    gen_bfv_hoisted(random.Random(0x42484F49))
     print("golden vectors written to", HERE)
 
 
@@ -187,5 +206,7 @@ if __name__ == "__main__":
         gen_bfv_hps(random.Random(0x485053))
     elif sys.argv[1:] == ["hoisted"]:
         gen_ckks_hoisted(random.Random(0x484F4953))
+    elif sys.argv[1:] == ["hoisted_bfv"]:
+        gen_bfv_hoisted(random.Random(0x42484F49))
     else:
         main()

@@ -62,6 +62,14 @@ def test_hoisted_golden(hb):
     assert np.array_equal(got[:, 0], g["out"])
 
 
+def test_bfv_hoisted_golden(hb):
+    g = np.load(os.path.join(GOLD, "bfv_hoisted_n1024_l4.npz"))
+    c = hb.Context(SCHEME_BFV, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), t=int(g["t"]),
+                   moduli=g["moduli"])
+    got = _run(hb, c, g["ct"][None], [int(x) for x in g["galois"]], list(g["gks"]))
+    assert np.array_equal(got[:, 0], g["out"])
+
+
 def test_hoisted_metric_params(hb, metric):
     o, c = metric
     ct = o.uniform((2, 2, o.L, o.n), seed=1100)

@@ -137,3 +137,11 @@ def test_ckks_hoisted_rotations_golden():
     out = o.rotate_hoisted(g["ct"][None], g["galois"], g["gks"])
     assert np.array_equal(out[:, 0], g["out"])
     assert np.array_equal(o.rotate_hoisted_at(g["ct"][None], g["galois"], g["gks"], o.L)[:, 0], g["out"])
+
+
+def test_bfv_hoisted_rotations_golden():
+    g = load("bfv_hoisted_n1024_l4.npz")
+    o = Oracle(SCHEME_BFV, int(g["log_n"]), int(g["L"]), int(g["K"]), int(g["dnum"]), t=int(g["t"]),
+               moduli=g["moduli"])
+    out = o.rotate_hoisted(g["ct"][None], g["galois"], g["gks"])
+    assert np.array_equal(out[:, 0], g["out"])
