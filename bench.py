@@ -716,6 +716,11 @@ def cpu_baseline_child(args):
     g = o.galois_elt(1)
     done, dt = timed(lambda: o.rotate(a, g, k), threads, 3.0)
     sec["C4_ckks_rotate_per_s"] = round(done / dt, 3)
+    gs = [o.galois_elt(s_) for s_ in (1, 2, -1, 5)]
+    k4 = np.stack([k] * len(gs))
+    done, dt = timed(lambda: o.rotate_hoisted(a, gs, k4), len(gs) * threads, 3.0)
+    sec["C4_ckks_rotate_hoisted4_rot_per_s"] = round(done / dt, 3)
+    del k4
     del a, b, k
     o3 = Oracle(SCHEME_BFV, 15, 8, 4, 2, t=65537)
     a3 = o3.uniform((threads, 2, 8, 1 << 15), seed=31)

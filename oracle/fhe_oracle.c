@@ -842,15 +842,17 @@ void orc_mul_relin(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const
 static void rotate_lvl(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
                        uint32_t n_ct, uint32_t lvl) {
   const size_t L = lvl, N = c->n, CT = 2 * L * N;
-  uint64_t *tmp = malloc(sizeof(uint64_t) * CT), *ks = malloc(sizeof(uint64_t) * CT);
-  for (uint32_t i = 0; i < n_ct; ++i) {
+  /* one ciphertext per thread, as the other batched ops */
+#pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
+  for (long i = 0; i < (long)n_ct; ++i) {
+    uint64_t *tmp = malloc(sizeof(uint64_t) * CT), *ks = malloc(sizeof(uint64_t) * CT);
     if (c->scheme == ORC_SCHEME_CKKS) orc_automorph_ntt(c, ct + i * CT, tmp, g, 2, (uint32_t)L);
     else orc_automorph_coef(c, ct + i * CT, tmp, g, 2, 0, (uint32_t)L);
     keyswitch_lvl(c, tmp + L * N, gk, ks, c->scheme == ORC_SCHEME_CKKS, lvl);
     orc_add(c, tmp, ks, out + i * CT, 1, 0, (uint32_t)L);
     memcpy(out + i * CT + L * N, ks + L * N, sizeof(uint64_t) * L * N);
+    free(tmp); free(ks);
   }
-  free(tmp); free(ks);
 }
 
 void orc_rotate(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
