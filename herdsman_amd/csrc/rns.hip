@@ -182,13 +182,14 @@ template <bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) ks_prep_kernel(const u64 *__restrict__ d, u32 d_stride,
                                                            u64 *__restrict__ dc, u64 *__restrict__ ext,
                                                            const ModInfo *mods, u32 L, u32 QP, u32 alpha, u32 ndig,
-                                                           u32 log_n) {
+                                                           u32 log_n, const u64 *dsc) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 ct = blockIdx.y / L, i = blockIdx.y % L, j = i / alpha;
   const size_t N = (size_t)1 << log_n;
   const ModInfo m = mods[i];
   const u64 x = d[((size_t)ct * d_stride + i) * N + k];
-  dc[((size_t)ct * L + i) * N + k] = x;
+  // dsc (fused BFV key switch): dc holds ModUp's scaled sources x (Q_j/q_i)^-1
+  dc[((size_t)ct * L + i) * N + k] = dsc ? csub63(mont_mul<SP>(x, dsc[i], m), m.q) : x;
   ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub63(mont_mul<SP>(x, m.r2, m), m.q);
 }
 
@@ -289,7 +290,7 @@ template <bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) bfv_moddown_kernel(const u64 *__restrict__ acc, const u64 *base, u64 *out,
                                                                const u64 *__restrict__ h, const u64 *pinv,
                                                                const ModInfo *mods, u32 L, u32 K, u32 QP,
-                                                               u32 log_n, u32 add_mask) {
+                                                               u32 log_n, u32 add_mask, u32 base_ginv) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 p = blockIdx.y / L, i = blockIdx.y % L;  // p = 2 ct + b
   const size_t N = (size_t)1 << log_n;
@@ -307,7 +308,19 @@ __global__ void __launch_bounds__(EW_BLOCK) bfv_moddown_kernel(const u64 *__rest
   const u64 cv = csub63(dot_cols<4, SP>(v, h0, h1, m), m.q);
   u64 ks = csub63(mont_mul<SP>(sub_mod(ap[(size_t)i * N], cv, m.q), pinv[i], m), m.q);
   const size_t o = ((size_t)p * L + i) * N + k;
-  if (add_mask & (1u << (p & 1))) ks = add_mod(ks, base[o], m.q);
+  if (add_mask & (1u << (p & 1))) {
+    u64 bv;
+    if (base_ginv) {
+      // the base read through the coefficient automorphism (rotation: sigma_g(c0)
+      // is never stored; the map of aut_rows_coef_kernel)
+      const u32 n = 1u << log_n, j0 = (u32)(((u64)k * base_ginv) & (2 * n - 1));
+      const u64 *bp = base + ((size_t)p * L + i) * N;
+      bv = j0 < n ? bp[j0] : (bp[j0 - n] ? m.q - bp[j0 - n] : 0);
+    } else {
+      bv = base[o];
+    }
+    ks = add_mod(ks, bv, m.q);
+  }
   out[o] = ks;
 }
 
@@ -318,7 +331,7 @@ template <bool SP, bool NTT>
 __global__ void __launch_bounds__(EW_BLOCK) automorph_ks_kernel(const u64 *__restrict__ ct_in, u64 *__restrict__ base,
                                                                 u64 *__restrict__ dc, u64 *__restrict__ ext, u32 g,
                                                                 const ModInfo *mods, u32 L, u32 QP, u32 alpha,
-                                                                u32 ndig, u32 log_n) {
+                                                                u32 ndig, u32 log_n, const u64 *dsc) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
   const u32 ct = blockIdx.y / L, i = blockIdx.y % L, j = i / alpha;
   const size_t N = (size_t)1 << log_n, LN = (size_t)L * N;
@@ -345,8 +358,8 @@ __global__ void __launch_bounds__(EW_BLOCK) automorph_ks_kernel(const u64 *__res
       y1 = x1 ? m.q - x1 : 0;
     }
   }
-  base[(size_t)ct * 2 * LN + (size_t)i * N + k] = y0;
-  dc[(size_t)ct * LN + (size_t)i * N + k] = y1;
+  if (base) base[(size_t)ct * 2 * LN + (size_t)i * N + k] = y0;
+  dc[(size_t)ct * LN + (size_t)i * N + k] = dsc ? csub63(mont_mul<SP>(y1, dsc[i], m), m.q) : y1;
   ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub63(mont_mul<SP>(y1, m.r2, m), m.q);
 }
 
@@ -688,9 +701,10 @@ int inner_impl(fhe_ctx *c, const u64 *ext, const u64 *ksk, u64 *acc, u32 n, u32 
 }
 
 template <bool SP>
-int ks_prep_impl(fhe_ctx *c, const u64 *d, u32 d_stride, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+int ks_prep_impl(fhe_ctx *c, const u64 *d, u32 d_stride, u64 *dc, u64 *ext, u32 n, u32 ndig,
+                 const u64 *dsc = nullptr) {
   hipLaunchKernelGGL((ks_prep_kernel<SP>), dim3(c->n / EW_BLOCK, n * c->L), dim3(EW_BLOCK), 0, c->stream, d, d_stride,
-                     dc, ext, c->d_mods, c->L, c->L + c->K, c->alpha, ndig, c->log_n);
+                     dc, ext, c->d_mods, c->L, c->L + c->K, c->alpha, ndig, c->log_n, dsc);
   return fhe_check(c, hipGetLastError(), "ks_prep_kernel");
 }
 
@@ -702,16 +716,17 @@ static u32 galois_inv(u32 g, u32 log_n) {
 }
 
 template <bool SP>
-int automorph_ks_impl(fhe_ctx *c, const u64 *ct, u64 *base, u64 *dc, u64 *ext, u32 g, u32 n, u32 ndig, bool ntt) {
+int automorph_ks_impl(fhe_ctx *c, const u64 *ct, u64 *base, u64 *dc, u64 *ext, u32 g, u32 n, u32 ndig, bool ntt,
+                      const u64 *dsc = nullptr) {
   dim3 grid(c->n / EW_BLOCK, n * c->L);
   const u32 QP = c->L + c->K;
   if (ntt) {
     hipLaunchKernelGGL((automorph_ks_kernel<SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, ct, base, dc, ext, g,
-                       c->d_mods, c->L, QP, c->alpha, ndig, c->log_n);
+                       c->d_mods, c->L, QP, c->alpha, ndig, c->log_n, dsc);
   } else {
     const u32 inv = galois_inv(g, c->log_n);
     hipLaunchKernelGGL((automorph_ks_kernel<SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, ct, base, dc, ext, inv,
-                       c->d_mods, c->L, QP, c->alpha, ndig, c->log_n);
+                       c->d_mods, c->L, QP, c->alpha, ndig, c->log_n, dsc);
   }
   return fhe_check(c, hipGetLastError(), "automorph_ks_kernel");
 }
@@ -936,13 +951,68 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   return rc ? rc : ks_finish(c, w, w.ext, ksk, base, out, n, add_mask, ntt_form, base_g, 0);
 }
 
+template <bool SP>
+static int bfv_moddown_impl(fhe_ctx *c, const u64 *acc, const u64 *base, u64 *out, u32 n, u32 add_mask,
+                            u32 base_ginv) {
+  const u32 L = c->L, per = std::max<u32>(1, kMaxGridY / L);
+  const size_t N = c->n, QP = c->L + c->K;
+  for (u32 p0 = 0; p0 < 2 * n; p0 += per) {
+    const u32 np = std::min(per, 2 * n - p0);
+    hipLaunchKernelGGL((bfv_moddown_kernel<SP>), dim3(c->n / EW_BLOCK, np * L), dim3(EW_BLOCK), 0, c->stream,
+                       acc + (size_t)p0 * QP * N, base + (size_t)p0 * L * N, out + (size_t)p0 * L * N, c->moddown.h,
+                       c->d_pinv, c->d_mods, L, c->K, (u32)QP, c->log_n, add_mask, base_ginv);
+    int rc = fhe_check(c, hipGetLastError(), "bfv_moddown_kernel");
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
+// BFV relinearisation at two-pass sizes (c->bfv_ks_fuse), the coefficient-
+// domain counterpart of keyswitch_run's fused CKKS path, on a prepared scratch
+// whose dc holds ModUp's SCALED sources (the floor's dsc) and whose ext holds
+// the own-digit limbs d R (coefficient form):
+//   ModUp of digit j inside the column pass of the NTT of its converted limbs
+//   (ntt_fwd_modup_launch), the own limbs' NTT, then INTT(acc) over every limb
+//   of Q u P with the inner product in its first pass (PRO_KSP over all
+//   limbs; the P limbs come out as ModDown's v_k, the Q limbs as plain
+//   coefficients), and ModDown + combine in one kernel (bfv_moddown_kernel):
+//   no ModUp, inner-product or conversion intermediate reaches HBM.
+// Split for hoisted rotations: bfv_ks_extend once per input, bfv_ks_finish per
+// key (ext_g: the inner product reads sigma_g(ext), PRO_KSPG; base_ginv: the
+// base is read as sigma_g(base) by the coefficient map, base apart from out).
+static bool bfv_fused(const fhe_ctx *c) { return c->bfv_ks_fuse && BFV_KS_FUSE; }
+static int bfv_ks_extend(fhe_ctx *c, const KsWs &w, u32 n) {
+  const u32 L = c->L, QP = L + c->K, N = c->n, ndig = w.ndig;
+  int rc;
+  for (u32 j = 0; j < ndig; ++j)
+    if ((rc = ntt_fwd_modup_launch(c, w.dc, w.ext, n, ndig, j))) return rc;
+  for (u32 j = 0; j < ndig; ++j) {
+    const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
+    if ((rc = ntt_launch(c, LimbMap{w.ext + (size_t)j * QP * N, ndig * QP, hi - lo, lo, hi - lo, 0, 0, n}, false,
+                         false, c->special)))
+      return rc;
+  }
+  return FHE_OK;
+}
+static int bfv_ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
+                         u32 ext_g = 0, u32 base_ginv = 0) {
+  int rc = ntt_inv_ksp_launch(c, w.acc, w.ext, ksk, n, w.ndig, ext_g, true);
+  return rc ? rc : SP_DISPATCH(c, bfv_moddown_impl, c, w.acc, base, out, n, add_mask, base_ginv);
+}
+static int bfv_ks_fused(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask) {
+  int rc = bfv_ks_extend(c, w, n);
+  return rc ? rc : bfv_ks_finish(c, w, ksk, base, out, n, add_mask);
+}
+
 // Hybrid key switching of an arbitrary input d ([n][d_stride limbs], the L
 // limbs first; NTT form iff ntt_form).  d must not alias out.
 int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u64 *base, u64 *out, u32 n,
                  u32 add_mask, bool ntt_form, u64 *ws) {
   const KsWs w = ks_layout(c, n, ws);
-  int rc = SP_DISPATCH(c, ks_prep_impl, c, d, d_stride, w.dc, w.ext, n, w.ndig);
+  const bool fused = !ntt_form && bfv_fused(c);
+  int rc = SP_DISPATCH(c, ks_prep_impl, c, d, d_stride, w.dc, w.ext, n, w.ndig, fused ? c->d_bfv_dscale : nullptr);
   if (rc) return rc;
+  if (fused) return bfv_ks_fused(c, w, ksk, base, out, n, add_mask);
   return keyswitch_run(c, w, ksk, base, out, n, add_mask, ntt_form);
 }
 
@@ -975,7 +1045,19 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
     if ((rc = ntt_inv_automorph_launch(c, ct, g, read_sigma ? nullptr : base, w.dc, w.ext, n, w.ndig))) return rc;
     return keyswitch_run(c, w, gk, read_sigma ? ct : base, out, n, 1u, true, true, read_sigma ? g : 0u);
   }
-  if ((rc = SP_DISPATCH(c, automorph_ks_impl, c, ct, base, w.dc, w.ext, g, n, w.ndig, ntt_form))) return rc;
+  if (!ntt_form && bfv_fused(c)) {
+    // BFV at two-pass sizes: the fused key switch; with out apart from ct,
+    // sigma(c0) is never stored (the ModDown kernel reads c0 through the
+    // coefficient map)
+    const u64 *ce = ct + (size_t)n * 2 * LN;
+    const bool apart = out + (size_t)n * 2 * LN <= ct || ce <= out;
+    if ((rc = SP_DISPATCH(c, automorph_ks_impl, c, ct, apart ? nullptr : base, w.dc, w.ext, g, n, w.ndig, false,
+                          c->d_bfv_dscale)))
+      return rc;
+    if ((rc = bfv_ks_extend(c, w, n))) return rc;
+    return bfv_ks_finish(c, w, gk, apart ? ct : base, out, n, 1u, 0, apart ? galois_inv(g, c->log_n) : 0);
+  }
+  if ((rc = SP_DISPATCH(c, automorph_ks_impl, c, ct, base, w.dc, w.ext, g, n, w.ndig, ntt_form, nullptr))) return rc;
   return keyswitch_run(c, w, gk, base, out, n, 1u, ntt_form);
 }
 
@@ -1037,8 +1119,8 @@ static int aut_rows(fhe_ctx *c, const u64 *src, u32 src_gs, u64 *dst, u32 dst_gs
 // the gather path (sigma_g inside the fused inner-product passes) needs only
 // the key-switch scratch; the generic one also sigma_g(ext) and sigma_g(c0)
 static bool hoisted_gather(const fhe_ctx *c) {
-  return c->params.scheme == FHE_SCHEME_CKKS && c->log_n > 14 &&
-         ks_fused_inner(c, (c->L + c->alpha - 1) / c->alpha, true);
+  if (c->params.scheme != FHE_SCHEME_CKKS) return bfv_fused(c);  // BFV: PRO_KSPG over all limbs
+  return c->log_n > 14 && ks_fused_inner(c, (c->L + c->alpha - 1) / c->alpha, true);
 }
 size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n) {
   const size_t N = c->n, L = c->L, QP = c->L + c->K, ndig = (c->L + c->alpha - 1) / c->alpha;
@@ -1066,11 +1148,22 @@ int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois,
   u64 *ext_g = w.conv + n * 2 * LN;      // [n][ndig][QP][N] (generic path)
   u64 *base = ext_g + n * w.ndig * QP * c->n;  // [n][2][L][N], poly 0 = sigma(c0) (generic path)
   const bool gather = hoisted_gather(c), ckks = c->params.scheme == FHE_SCHEME_CKKS;
+  if (!ckks && gather) {
+    // BFV on the fused passes: scaled ModUp sources, one extension, then per
+    // element the gathered all-limb inner product and the coefficient-domain
+    // ModDown reading c0 through the coefficient map
+    if ((rc = SP_DISPATCH(c, ks_prep_impl, c, ct + LN, 2 * c->L, w.dc, w.ext, n, w.ndig, c->d_bfv_dscale))) return rc;
+    if ((rc = bfv_ks_extend(c, w, n))) return rc;
+    for (u32 r = 0; r < n_rot; ++r)
+      if ((rc = bfv_ks_finish(c, w, gks[r], ct, outs[r], n, 1u, galois[r], galois_inv(galois[r], c->log_n))))
+        return rc;
+    return FHE_OK;
+  }
   if (ckks && c->log_n > 14) {
     // the identity automorphism: INTT(c1) with the ModUp source scaling and
     // the own-digit slots c1 R, as rotate_impl's fused prologue
     if ((rc = ntt_inv_automorph_launch(c, ct, 1u, nullptr, w.dc, w.ext, n, w.ndig))) return rc;
-  } else if ((rc = SP_DISPATCH(c, ks_prep_impl, c, ct + LN, 2 * c->L, w.dc, w.ext, n, w.ndig))) {
+  } else if ((rc = SP_DISPATCH(c, ks_prep_impl, c, ct + LN, 2 * c->L, w.dc, w.ext, n, w.ndig, nullptr))) {
     return rc;
   }
   if ((rc = ks_extend(c, w, n, ckks, ckks && c->log_n > 14))) return rc;
@@ -1252,45 +1345,6 @@ int hps_setup(fhe_ctx *c) {
   return c->hps ? FHE_OK : FHE_ERR_OOM;
 }
 
-template <bool SP>
-static int bfv_moddown_impl(fhe_ctx *c, const u64 *acc, const u64 *base, u64 *out, u32 n, u32 add_mask) {
-  const u32 L = c->L, per = std::max<u32>(1, kMaxGridY / L);
-  const size_t N = c->n, QP = c->L + c->K;
-  for (u32 p0 = 0; p0 < 2 * n; p0 += per) {
-    const u32 np = std::min(per, 2 * n - p0);
-    hipLaunchKernelGGL((bfv_moddown_kernel<SP>), dim3(c->n / EW_BLOCK, np * L), dim3(EW_BLOCK), 0, c->stream,
-                       acc + (size_t)p0 * QP * N, base + (size_t)p0 * L * N, out + (size_t)p0 * L * N, c->moddown.h,
-                       c->d_pinv, c->d_mods, L, c->K, (u32)QP, c->log_n, add_mask);
-    int rc = fhe_check(c, hipGetLastError(), "bfv_moddown_kernel");
-    if (rc) return rc;
-  }
-  return FHE_OK;
-}
-
-// BFV relinearisation at two-pass sizes (c->bfv_ks_fuse), the coefficient-
-// domain counterpart of keyswitch_run's fused CKKS path, on a prepared scratch
-// whose dc holds ModUp's SCALED sources (the floor's dsc) and whose ext holds
-// the own-digit limbs d R (coefficient form):
-//   ModUp of digit j inside the column pass of the NTT of its converted limbs
-//   (ntt_fwd_modup_launch), the own limbs' NTT, then INTT(acc) over every limb
-//   of Q u P with the inner product in its first pass (PRO_KSP over all
-//   limbs; the P limbs come out as ModDown's v_k, the Q limbs as plain
-//   coefficients), and ModDown + combine in one kernel (bfv_moddown_kernel):
-//   no ModUp, inner-product or conversion intermediate reaches HBM.
-static int bfv_ks_fused(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask) {
-  const u32 L = c->L, QP = L + c->K, N = c->n, ndig = w.ndig;
-  int rc;
-  for (u32 j = 0; j < ndig; ++j)
-    if ((rc = ntt_fwd_modup_launch(c, w.dc, w.ext, n, ndig, j))) return rc;
-  for (u32 j = 0; j < ndig; ++j) {
-    const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
-    if ((rc = ntt_launch(c, LimbMap{w.ext + (size_t)j * QP * N, ndig * QP, hi - lo, lo, hi - lo, 0, 0, n}, false,
-                         false, c->special)))
-      return rc;
-  }
-  if ((rc = ntt_inv_ksp_launch(c, w.acc, w.ext, ksk, n, ndig, 0, true))) return rc;
-  return SP_DISPATCH(c, bfv_moddown_impl, c, w.acc, base, out, n, add_mask);
-}
 
 size_t bfv_mul_ws_bytes(const fhe_ctx *c, u32 n) {
   const size_t N = c->n, L = c->L, nB = c->nB;
@@ -1324,7 +1378,7 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   if ((rc = ntt_inv_bfv_tensor_launch(c, xb, xb + (size_t)n * 2 * nB * N, eb, nB, bsk0, n))) return rc;
   // 5. scale and round: r0, r1 -> out; r2 -> the key-switch scratch, prepared
   //    (BEHZ floor, or HPS simple scaling + exact P -> Q)
-  const u64 *dsc = c->bfv_ks_fuse && BFV_KS_FUSE ? c->d_bfv_dscale : nullptr;
+  const u64 *dsc = bfv_fused(c) ? c->d_bfv_dscale : nullptr;
   if ((rc = c->hps ? SP_DISPATCH(c, hps_scale_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig, dsc)
                    : SP_DISPATCH(c, behz_floor_impl, c, eq, eb, out, w.dc, w.ext, n, w.ndig, dsc)))
     return rc;

@@ -88,3 +88,27 @@ def test_sweep(hb, i, scheme, log_n, L, K, dnum, generic, mult):
         ol = hb.empty((nct, 2, lvl, n))
         c.mul_relin_at(hb.to_device(al), hb.to_device(bl), dk, ol, lvl)
         assert np.array_equal(hb.to_host(ol), o.mul_relin_at(al, bl, k, lvl)), ("mul_relin_at", lvl)
+
+
+@pytest.mark.parametrize("log_n,L,K,dnum", [(15, 8, 4, 2), (16, 3, 2, 3)])
+def test_bfv_fused_key_switch_paths(hb, log_n, L, K, dnum):
+    """BFV at two-pass sizes runs every key switch on the fused passes (ModUp in
+    the NTT column pass, the all-limb inner product in INTT(acc)'s first pass,
+    one ModDown kernel): keyswitch, rotate apart (c0 read through the
+    coefficient map) and in place (sigma(c0) stored first)."""
+    o = Oracle(SCHEME_BFV, log_n, L, K, dnum, t=65537)
+    c = hb.Context(SCHEME_BFV, log_n, L, K, dnum, t=65537, moduli=o.moduli)
+    a = o.uniform((2, 2, L, o.n), seed=9100 + log_n)
+    k = o.uniform(o.key_shape(), seed=9101)
+    dk = hb.to_device(k)
+    g = o.galois_elt(-2)
+    want = o.rotate(a, g, k)
+    out = hb.empty((2, 2, L, o.n))
+    c.rotate(hb.to_device(a), g, dk, out)
+    assert np.array_equal(hb.to_host(out), want)
+    io = hb.to_device(a)
+    c.rotate(io, g, dk, io)
+    assert np.array_equal(hb.to_host(io), want)
+    d = o.uniform((2, L, o.n), seed=9102)
+    c.keyswitch(hb.to_device(d), dk, out)
+    assert np.array_equal(hb.to_host(out), o.keyswitch(d, k))
