@@ -278,6 +278,9 @@ def main():
     ctx.fill_uniform(x, seed=99)
     for _ in range(3):
         ctx.ntt_fwd(x)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()  # every rank's NTT loop runs at the same time (the N-GPU NTT/s)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)  # the stream the NTT kernels are launched on (ctx.set_stream above)
     reps = max(1, args.ntt_reps)
@@ -287,6 +290,10 @@ def main():
     e1.synchronize()
     ntt_ms = e0.elapsed_time(e1) / reps
     del x
+    ntt_rates = [limbs / (ntt_ms * 1e-3)]
+    if world > 1:
+        ntt_rates = [None] * world
+        dist.all_gather_object(ntt_rates, limbs / (ntt_ms * 1e-3))
     algo_per_limb = 2 * n * 8
     algo_bytes = limbs * algo_per_limb
     achieved = algo_bytes / (ntt_ms * 1e-3) / 1e9
@@ -338,6 +345,9 @@ def main():
             },
             "roofline": roof,
             "ntt_fwd_limb_per_s": round(limbs / (ntt_ms * 1e-3), 1),
+            # all ranks' NTT loops at once (N=2^16 limb-NTTs per second over the node)
+            "ntt_fwd_limb_per_s_all_gpus": round(sum(ntt_rates), 1),
+            "ntt_fwd_limb_per_s_per_rank": [round(v, 1) for v in ntt_rates],
             "per_rank_ct_mult_per_s": [round(v, 1) for v in per_rank],
             "key_bcast_ms": round(key_bcast_ms, 3),
             "key_bcast_via": bcast,
