@@ -16,6 +16,7 @@
 #   optrace=OP     rocprofv3 --kernel-trace --stats of tools/op_bench.py OP (bfv_mul, ckks_mul, ckks_rot)
 #   prof           tools/profile_round.sh (roofline stats, PMC passes; summarise with tools/collect_profile.py)
 #   steptable      rocprofv3 kernel trace of one C5 wave loop -> tools/step_table.py
+#   wgbench        GpuWorkerGroup MapTask throughput end to end (wg_run bench, files under /tmp on the box)
 set -e
 export TMPDIR=/tmp
 O=$1; shift
@@ -51,6 +52,7 @@ for s in "$@"; do
       timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/st_write" -o run -- $B --reps 2 > "$O/st_write.log" 2>&1 ;;
     optrace=*) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/op_${s#optrace=}" -o run -- python3 tools/op_bench.py "${s#optrace=}" --batch 128 --reps 5 > "$O/op_${s#optrace=}.log" 2>&1 ;;
     prof) timeout -k 10 1100 bash tools/profile_round.sh "$O/prof" > "$O/prof.log" 2>&1 ;;
+    wgbench) rm -rf /tmp/wgb && timeout -k 10 400 herdsman_amd/bin/wg_run bench /tmp/wgb 0,16,12,4,3,0 4 64 4 16 6 > "$O/wg_bench.log" 2>&1; rm -rf /tmp/wgb ;;
     steptable) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/step" -o run -- python3 tools/op_bench.py ckks_mul --batch 128 --reps 8 > "$O/step.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
