@@ -1099,6 +1099,7 @@ __global__ void __launch_bounds__(EW_BLOCK) aut_rows_coef_kernel(const u64 *__re
 static int aut_rows(fhe_ctx *c, const u64 *src, u32 src_gs, u64 *dst, u32 dst_gs, u32 rpg, u32 n_rows, u32 g,
                     bool coef = false) {
   const u32 per = kMaxGridY / rpg * rpg;
+  if (!per) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "aut_rows: rows per group exceed the grid");
   const size_t N = c->n;
   for (u32 r0 = 0; r0 < n_rows; r0 += per) {
     const u32 nr = std::min(per, n_rows - r0), g0 = r0 / rpg;
