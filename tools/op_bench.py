@@ -1,6 +1,9 @@
 """Time one ciphertext op at a BASELINE config (GPU box), for rocprofv3 runs.
 
-    python tools/op_bench.py bfv_mul|ckks_mul|ckks_rot [--batch 32] [--reps 10] [--openfhe-primes]
+    python tools/op_bench.py bfv_mul|ckks_mul|ckks_rot|ckks_hrot|bfv_rot|bfv_hrot [--batch 32] [--reps 10]
+                             [--openfhe-primes]
+
+*_hrot: 4 hoisted rotations of the batch (fhe_rotate_hoisted); the rate counts rotations.
 
 --openfhe-primes: the CKKS ops on OpenFHE-style primes (q = 1 mod 2N, generic
 Montgomery path) instead of the default q = 1 (mod 2^32) family.
@@ -15,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("op", choices=["bfv_mul", "ckks_mul", "ckks_rot"])
+    ap.add_argument("op", choices=["bfv_mul", "ckks_mul", "ckks_rot", "ckks_hrot", "bfv_rot", "bfv_hrot"])
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--openfhe-primes", action="store_true")
@@ -23,7 +26,7 @@ def main():
     import torch
     import herdsman_amd.backend as hb
 
-    if args.op == "bfv_mul":
+    if args.op.startswith("bfv"):
         c = hb.Context(hb.SCHEME_BFV, 15, 8, 4, 2, t=65537)
     else:
         mods = None
@@ -39,8 +42,13 @@ def main():
     k = c.fill_uniform(hb.empty(c.key_shape()), seed=3)
     out = hb.empty(shape)
     g = c.galois_elt(1)
+    gs = [c.galois_elt(s_) for s_ in (1, 2, -1, 5)]
+    outs = [hb.empty(shape) for _ in gs] if args.op.endswith("hrot") else []
+    per = len(gs) if args.op.endswith("hrot") else 1
     fn = {"bfv_mul": lambda: c.mul_relin(a, b, k, out), "ckks_mul": lambda: c.mul_relin(a, b, k, out),
-          "ckks_rot": lambda: c.rotate(a, g, k, out)}[args.op]
+          "ckks_rot": lambda: c.rotate(a, g, k, out), "bfv_rot": lambda: c.rotate(a, g, k, out),
+          "ckks_hrot": lambda: c.rotate_hoisted(a, gs, [k] * len(gs), outs),
+          "bfv_hrot": lambda: c.rotate_hoisted(a, gs, [k] * len(gs), outs)}[args.op]
     fn()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -48,7 +56,7 @@ def main():
         fn()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.reps
-    print(f"{args.op}: {dt * 1e3:.3f} ms per call of {args.batch} -> {args.batch / dt:.1f} ops/s")
+    print(f"{args.op}: {dt * 1e3:.3f} ms per call of {args.batch} -> {per * args.batch / dt:.1f} ops/s")
 
 
 if __name__ == "__main__":
