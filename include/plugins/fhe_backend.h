@@ -147,9 +147,11 @@ int fhe_rotate(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const uint
  * EvalFastRotation, which herdsman's linked library provides for rotation-heavy
  * circuits).  galois_elts, gks, outs: HOST arrays of n_rot entries; gks[r] is a
  * device Galois key for galois_elts[r], outs[r] a device [n_ct][2][L][N]
- * buffer that must not overlap ct or another outs[q].  outs[r] = (sigma(c0) + KS_0, KS_1) with KS
- * over sigma_g(ModUp(c1)): decrypts like fhe_rotate's result, but the bits
- * differ from it by the ModUp error term (oracle orc_rotate_hoisted). */
+ * buffer that must not overlap ct or another outs[q].  outs[r] =
+ * (sigma(c0) + KS_0, KS_1) with KS over sigma_g(ModUp(c1)): decrypts like
+ * fhe_rotate's result, but the bits differ from it by the ModUp error term
+ * (oracle orc_rotate_hoisted).  CKKS in the NTT domain, BFV in the
+ * coefficient domain, as the other ciphertext ops. */
 int fhe_rotate_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
                        const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct);
 /* 5^steps mod 2N (steps may be negative); conjugation is 2N-1 */
