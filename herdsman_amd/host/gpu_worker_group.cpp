@@ -674,7 +674,7 @@ LaneSchema &lane_schema(std::map<int, std::unique_ptr<LaneSchema>> &m, const Gpu
   s.q_digest = moduli_digest(s.moduli.data(), s.L);
   s.qp_digest = moduli_digest(s.moduli.data(), s.L + s.K);
   s.level_digest.resize(s.L + 1);
-  for (uint32_t m = 1; m <= s.L; ++m) s.level_digest[m] = moduli_digest(s.moduli.data(), m);
+  for (uint32_t lv = 1; lv <= s.L; ++lv) s.level_digest[lv] = moduli_digest(s.moduli.data(), lv);
   auto &slot = m[schema];
   slot = std::move(ls);
   // the lane's own stream: lanes of one device run concurrently
@@ -1023,7 +1023,7 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
           if (mul) ck(s.ctx, fhe_mul_relin_at(s.ctx, older.p, newer.p, rlk, newer.p, 1, level), "reduce merge");
           else ck(s.ctx, fhe_add_at(s.ctx, older.p, newer.p, newer.p, 1, level), "reduce merge");
         };
-        ArenaBuf dev[2] = {ArenaBuf(*ls.arena, C * cw), ArenaBuf(*ls.arena, C * cw)};
+        ArenaBuf stage[2] = {ArenaBuf(*ls.arena, C * cw), ArenaBuf(*ls.arena, C * cw)};
         bool used[2] = {false, false};
         size_t pi = 0, ri = 0, k = 0;
         while (pi < parts.size() && parts[pi]->size() == 0) ++pi;
@@ -1045,11 +1045,11 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
               while (pi < parts.size() && parts[pi]->size() == 0) ++pi;
             }
           }
-          ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, dev[si].p, host, m * cw * 8), "h2d");
+          ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, stage[si].p, host, m * cw * 8), "h2d");
           ck(s.ctx, fhe_mark(s.ctx, (uint32_t)si), "reduce slot mark");
           used[si] = true;
           Partial p{ArenaBuf(*ls.arena, cw), 0};
-          ck(s.ctx, fhe_reduce_at(s.ctx, dev[si].p, (uint32_t)m, op, rlk, p.buf.p, level), "reduce");
+          ck(s.ctx, fhe_reduce_at(s.ctx, stage[si].p, (uint32_t)m, op, rlk, p.buf.p, level), "reduce");
           while (!pend.empty() && pend.back().height == p.height) {
             combine(pend.back().buf, p.buf);
             p.height += 1;
