@@ -5,7 +5,8 @@ sweep draws (log_n, L, K, dnum, scheme, BFV technique, prime family) from a
 fixed seed so that partial last digits, alpha not dividing L, K < alpha,
 one-pass and two-pass sizes, both lazy-schedule classes and both BFV
 multiplication techniques meet every op: mul+relin, rotate, keyswitch,
-hoisted rotations, and for CKKS rescale and a level-reduced mul+relin.
+hoisted rotations, and for CKKS rescale, a level-reduced mul+relin and
+level-reduced hoisted rotations.
 """
 import random
 
@@ -88,6 +89,11 @@ def test_sweep(hb, i, scheme, log_n, L, K, dnum, generic, mult):
         ol = hb.empty((nct, 2, lvl, n))
         c.mul_relin_at(hb.to_device(al), hb.to_device(bl), dk, ol, lvl)
         assert np.array_equal(hb.to_host(ol), o.mul_relin_at(al, bl, k, lvl)), ("mul_relin_at", lvl)
+        hl = [hb.empty((nct, 2, lvl, n)) for _ in gs]
+        c.rotate_hoisted_at(hb.to_device(al), gs, [dk, dk], hl, lvl)
+        want = o.rotate_hoisted_at(al, gs, np.stack([k, k]), lvl)
+        for r in range(len(gs)):
+            assert np.array_equal(hb.to_host(hl[r]), want[r]), ("hoisted_at", lvl, r)
 
 
 @pytest.mark.parametrize("log_n,L,K,dnum", [(15, 8, 4, 2), (16, 3, 2, 3)])
