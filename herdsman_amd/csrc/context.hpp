@@ -11,6 +11,7 @@
 
 #define FHE_MAX_MODS 48
 #define FHE_MAX_CONV_SRC 16
+#define FHE_ROT_BATCH 8  // Galois elements per launch of the rotation-batched gather passes
 
 // gridDim.y of the per-coefficient kernels holds (item, limb); every launch
 // keeps it below this bound
@@ -188,10 +189,18 @@ struct ConvSrc {
   u64 lift_half;       // 0: plain conversion
   const u64 *lift_sub;  // [nd] device
 };
+// Hoisted rotations of few ciphertexts: nr Galois elements' gather passes in
+// one launch (poly p of the batch = rotation p / (2 n), ciphertext poly p % (2 n))
+struct RotBatch {
+  u32 nr;
+  const u64 *ksk[FHE_ROT_BATCH];
+  u64 *out[FHE_ROT_BATCH];
+  u32 g[FHE_ROT_BATCH];
+};
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro = nullptr, const u64 *ext = nullptr,
                            const u64 *ksk = nullptr, u32 ndig = 0, u32 base_g = 0, const u64 *pinv = nullptr,
-                           const ConvSrc *pro_src = nullptr, u32 ext_g = 0);
+                           const ConvSrc *pro_src = nullptr, u32 ext_g = 0, const RotBatch *rb = nullptr);
 // ModUp of digit j fused into the column pass of the forward NTT of its
 // converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
@@ -202,7 +211,7 @@ int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, 
 // (ext_g != 0: ext is read as sigma_g(ext), the hoisted rotation's inner product)
 // (all_limbs: every Q u P limb with the output constants d_bfv_kscale, BFV)
 int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, u32 ext_g = 0,
-                       bool all_limbs = false);
+                       bool all_limbs = false, const RotBatch *rb = nullptr);
 // (base null: sigma(c0) is not stored; the combine then reads it with base_g)
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);

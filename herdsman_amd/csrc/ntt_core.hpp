@@ -106,6 +106,14 @@ struct NttArgs {
   u32 e_ndig, e_QP;
   u32 e_kQP, e_kshift;  // key rows per digit half; key row of limb i >= L is i + e_kshift (level views)
   u32 e_ext_g;          // EPI_KSQG / PRO_KSPG: ext is read as sigma_g(ext) (hoisted rotation)
+  // EPI_KSQG / PRO_KSPG over several Galois elements in one launch (hoisted
+  // rotations of few ciphertexts): poly p belongs to rotation r = p / e_rp and
+  // ciphertext poly p % e_rp; rotation r's key, element and output replace
+  // e_ksk, e_ext_g / e_g and e_out.  e_rp = 0: one rotation.
+  u32 e_rp;
+  const u64 *e_ksk_r[FHE_ROT_BATCH];
+  u64 *e_out_r[FHE_ROT_BATCH];
+  u32 e_g_r[FHE_ROT_BATCH];
   // PRO_TENSOR (first pass of the inverse NTT of d2 in CKKS mul+relin, poly =
   // ciphertext): the pass reads the operands a, b [ct][2][L][N] instead of d2,
   // writes the relinearisation base out[ct][0] = a0 b0, out[ct][1] = a0 b1 + a1 b0
@@ -196,6 +204,7 @@ struct EpiRow {
   const u64 *a0, *a1, *b0, *b1;  // PRO_TENSOR
   u64 *o0, *o1, *ext;
   u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base or null; ext); combine: e_g
+  u32 xg;  // EPI_KSQG / PRO_KSPG: the Galois element ext is gathered through
   u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is
   const u64 *src;  // PRO_CONV: source limb 0 of this poly (limb i at src + i N)
   u64 h[4];        // PRO_CONV: h[i][m] of this workgroup's target limb
@@ -485,7 +494,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
 #pragma unroll
         for (int r = 0; r < PD; ++r) {
           const u32 kr = Grp<S, LOGR, 0>::k_reg(r);
-          const u32 eo = ksq_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kr, a.e_ext_g) : voff;
+          const u32 eo = ksq_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kr, ep.xg) : voff;
 #pragma unroll
           for (int j = 0; j < KD; ++j) {
             ek[r][j] = ld_b(ep.kext + (ksq_gather(EPI) ? 0 : kr) + j * ep.ext_j, eo);
@@ -519,7 +528,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
             // the lazy sum below 4q; otherwise it is made canonical.
             if (r + PD < R) {
               const u32 kn = G0::k_reg(r + PD);
-              const u32 eo = ksq_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kn, a.e_ext_g) : voff;
+              const u32 eo = ksq_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kn, ep.xg) : voff;
 #pragma unroll
               for (int j = 0; j < KD; ++j) {
                 ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + (ksq_gather(EPI) ? 0 : kn) + j * ep.ext_j, eo);
@@ -678,7 +687,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 #pragma unroll
       for (int r = 0; r < PD; ++r) {
         const u32 kr = GZ::k_reg(r);
-        const u32 eo = ksp_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kr, a.e_ext_g) : voff;
+        const u32 eo = ksp_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kr, ep.xg) : voff;
 #pragma unroll
         for (int j = 0; j < KD; ++j) {
           ek[r][j] = ld_b(ep.kext + (ksp_gather(EPI) ? 0 : kr) + j * ep.ext_j, eo);
@@ -689,7 +698,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       for (int r = 0; r < R; ++r) {
         if (r + PD < R) {
           const u32 kn = GZ::k_reg(r + PD);
-          const u32 eo = ksp_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kn, a.e_ext_g) : voff;
+          const u32 eo = ksp_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kn, ep.xg) : voff;
 #pragma unroll
           for (int j = 0; j < KD; ++j) {
             ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + (ksp_gather(EPI) ? 0 : kn) + j * ep.ext_j, eo);
@@ -885,28 +894,41 @@ __global__ void __launch_bounds__(W << (S - LOGR),
   const u32 gb = (hi << (S + PG::LS)) + (u & (stride - 1));
 
   EpiRow ep{};
+  // rotation-batched gather passes: this poly's rotation and ciphertext poly
+  u32 rot = 0, cpoly = poly;
+  const u64 *ksk = a.e_ksk;
+  if constexpr (ksq_gather(EPI) || ksp_gather(EPI)) {
+    ep.xg = a.e_ext_g;
+    if (a.e_rp) {
+      rot = poly / a.e_rp;
+      cpoly = poly - rot * a.e_rp;
+      ksk = a.e_ksk_r[rot];
+      ep.xg = a.e_g_r[rot];
+    }
+  }
   if constexpr (is_ksp(EPI)) {
     // P limbs: key row limb + e_kshift (a level view reads the full-level key)
     const size_t N = (size_t)1 << LOG_N;
     ep.ext_j = (size_t)a.e_QP * N;
     ep.ksk_j = (size_t)2 * a.e_kQP * N;
-    ep.kext = a.e_ext + ((size_t)(poly >> 1) * a.e_ndig * a.e_QP + limb) * N;
-    ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_kQP + limb + a.e_kshift) * N;
+    ep.kext = a.e_ext + ((size_t)(cpoly >> 1) * a.e_ndig * a.e_QP + limb) * N;
+    ep.kksk = ksk + ((size_t)(cpoly & 1) * a.e_kQP + limb + a.e_kshift) * N;
   }
   if constexpr (is_combine(EPI)) {
     if constexpr (is_ksq(EPI)) {
       const size_t N = (size_t)1 << LOG_N;
       ep.ext_j = (size_t)a.e_QP * N;
       ep.ksk_j = (size_t)2 * a.e_kQP * N;
-      ep.kext = a.e_ext + ((size_t)(poly >> 1) * a.e_ndig * a.e_QP + limb) * N;
-      ep.kksk = a.e_ksk + ((size_t)(poly & 1) * a.e_kQP + limb) * N;  // Q limbs: key row = limb
+      ep.kext = a.e_ext + ((size_t)(cpoly >> 1) * a.e_ndig * a.e_QP + limb) * N;
+      ep.kksk = ksk + ((size_t)(cpoly & 1) * a.e_kQP + limb) * N;  // Q limbs: key row = limb
     }
     ep.acc = a.e_acc + (((size_t)poly * a.e_acc_stride + limb) << LOG_N);
-    ep.base = a.e_base + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
-    ep.out = a.e_out + (((size_t)poly * a.map.poly_stride + limb) << LOG_N);
+    ep.base = a.e_base + (((size_t)cpoly * a.map.poly_stride + limb) << LOG_N);
+    ep.out = (ksq_gather(EPI) && a.e_rp ? a.e_out_r[rot] : a.e_out) +
+             (((size_t)cpoly * a.map.poly_stride + limb) << LOG_N);
     ep.pinv = a.e_pinv[limb];
     ep.add = (a.e_add_mask >> (poly & 1)) & 1;
-    ep.g = a.e_g;
+    ep.g = ksq_gather(EPI) && a.e_rp ? a.e_g_r[rot] : a.e_g;
   }
   if constexpr (EPI == PRO_TENSOR) {
     const size_t LN = (size_t)a.t_L << LOG_N;

@@ -65,7 +65,7 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
 // stored, the P rows of acc receive INTT(acc_P) times d_iscale (ModDown's
 // source constants, as ntt_launch(..., d_iscale) gives them)
 int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, u32 ext_g,
-                       bool all_limbs) {
+                       bool all_limbs, const RotBatch *rb) {
   const u32 L = c->L, K = c->K, QP = L + K;
   const size_t N = c->n;
   if (c->log_n <= 14 || ndig < 1 || ndig > 4)
@@ -73,9 +73,13 @@ int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32
   if (all_limbs && (!c->d_bfv_kscale || c->key_pshift))
     return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused all-limb inner product: BFV tables");
   const u32 l0 = all_limbs ? 0 : L, nl = all_limbs ? QP : K;
+  // rb: acc holds rb->nr rotations' accumulators of the n ciphertexts, one chunk
+  const u32 nr = rb ? rb->nr : 1;
+  if (rb && (nr < 1 || nr > FHE_ROT_BATCH || 2 * n * nr > 65534u))
+    return fhe_fail(c, FHE_ERR_INVALID, "rotation batch: count / size");
   const u32 per = 65534u;  // gridDim.y, even (the polys of a ciphertext stay together)
-  for (u32 p0 = 0; p0 < 2 * n; p0 += per) {
-    const u32 np = std::min(per, 2 * n - p0);
+  for (u32 p0 = 0; p0 < 2 * n * nr; p0 += per) {
+    const u32 np = std::min(per, 2 * n * nr - p0);
     NttArgs a{};
     a.map = LimbMap{acc + (size_t)p0 * QP * N, QP, nl, l0, QP, 0, 0, np};
     a.tw = c->d_tw_inv;
@@ -90,9 +94,16 @@ int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32
     a.e_kQP = ctx_key_qp(c);
     a.e_kshift = c->key_pshift;
     a.e_ext_g = ext_g & ((2u << c->log_n) - 1);
+    if (rb) {
+      a.e_rp = 2 * n;
+      for (u32 r = 0; r < nr; ++r) {
+        a.e_ksk_r[r] = rb->ksk[r];
+        a.e_g_r[r] = rb->g[r] & ((2u << c->log_n) - 1);
+      }
+    }
     const u32 n_jobs = np * nl;
     int rc;
-    switch (ndig + (ext_g ? 4 : 0)) {
+    switch (ndig + (ext_g || rb ? 4 : 0)) {
       case 1: rc = row_pass<PRO_KSP>(c, a, true, n_jobs); break;
       case 2: rc = row_pass<PRO_KSP + 1>(c, a, true, n_jobs); break;
       case 3: rc = row_pass<PRO_KSP + 2>(c, a, true, n_jobs); break;

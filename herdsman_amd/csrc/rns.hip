@@ -1123,8 +1123,19 @@ static bool hoisted_gather(const fhe_ctx *c) {
   if (c->params.scheme != FHE_SCHEME_CKKS) return bfv_fused(c);  // BFV: PRO_KSPG over all limbs
   return c->log_n > 14 && ks_fused_inner(c, (c->L + c->alpha - 1) / c->alpha, true);
 }
+// CKKS gather path with few ciphertexts: up to FHE_ROT_BATCH Galois elements
+// per launch of the gather passes, while the batch stays within ROT_BATCH_CTS
+// ciphertexts' accumulators (a launch over one ciphertext fills 1.5 workgroups
+// per CU; hoisting's common case is one ciphertext and many rotations)
+constexpr u32 ROT_BATCH_CTS = 32;
+static u32 hoisted_rot_batch(const fhe_ctx *c, u32 n) {
+  if (c->params.scheme != FHE_SCHEME_CKKS || !hoisted_gather(c)) return 1;
+  return std::max<u32>(1, std::min<u32>(FHE_ROT_BATCH, ROT_BATCH_CTS / std::max<u32>(n, 1)));
+}
 size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n) {
   const size_t N = c->n, L = c->L, QP = c->L + c->K, ndig = (c->L + c->alpha - 1) / c->alpha;
+  const size_t nrb = hoisted_rot_batch(c, n);
+  if (nrb > 1) return keyswitch_ws_bytes(c, n) + sizeof(u64) * N * n * nrb * (2 * QP + 2 * L);
   return keyswitch_ws_bytes(c, n) + (hoisted_gather(c) ? 0 : sizeof(u64) * N * n * (ndig * QP + 2 * L));
 }
 
@@ -1168,6 +1179,27 @@ int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois,
     return rc;
   }
   if ((rc = ks_extend(c, w, n, ckks, ckks && c->log_n > 14))) return rc;
+  const u32 nrb = hoisted_rot_batch(c, n);
+  if (nrb > 1) {
+    // several Galois elements per launch: accumulators and conversions of the
+    // batch after the key-switch scratch
+    const u32 ndig = w.ndig;
+    u64 *accb = w.conv + (size_t)n * 2 * LN, *convb = accb + (size_t)nrb * n * 2 * QP * c->n;
+    for (u32 r0 = 0; r0 < n_rot; r0 += nrb) {
+      RotBatch rb{};
+      rb.nr = std::min(nrb, n_rot - r0);
+      for (u32 r = 0; r < rb.nr; ++r) {
+        rb.ksk[r] = gks[r0 + r];
+        rb.out[r] = outs[r0 + r];
+        rb.g[r] = galois[r0 + r];
+      }
+      if ((rc = ntt_inv_ksp_launch(c, accb, w.ext, nullptr, n, ndig, 0, false, &rb))) return rc;
+      if ((rc = ntt_fwd_combine_launch(c, convb, 2 * n * rb.nr, accb, (u32)QP, ct, nullptr, 1u, &c->moddown, w.ext,
+                                       nullptr, ndig, 0, nullptr, nullptr, 0, &rb)))
+        return rc;
+    }
+    return FHE_OK;
+  }
   for (u32 r = 0; r < n_rot; ++r) {
     const u32 g = galois[r];
     if (gather) {

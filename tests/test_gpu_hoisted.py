@@ -84,6 +84,19 @@ def test_hoisted_metric_params(hb, metric):
     assert not np.array_equal(plain, want[0, :1])
 
 
+@pytest.mark.parametrize("n_ct,steps", [(1, (1, 2, 3, 4, 5, 6, 7, -1, -2, -3)), (16, (1, -1, 3))])
+def test_hoisted_rotation_batches(hb, metric, n_ct, steps):
+    """Few ciphertexts: several Galois elements per launch of the gather passes
+    (FHE_ROT_BATCH = 8 per launch while n_ct * batch <= 32): 10 elements on one
+    ciphertext run as 8 + 2, 3 elements on 16 ciphertexts as 2 + 1."""
+    o, c = metric
+    ct = o.uniform((n_ct, 2, o.L, o.n), seed=1600 + n_ct)
+    gs = [o.galois_elt(k) for k in steps]
+    gks = [o.uniform(o.key_shape(), seed=1610 + i) for i in range(len(gs))]
+    want = o.rotate_hoisted(ct, gs, np.stack(gks))
+    assert np.array_equal(_run(hb, c, ct, gs, gks), want)
+
+
 @pytest.mark.parametrize("lvl", [7, 5])
 def test_hoisted_at_levels(hb, metric, lvl):
     o, c = metric

@@ -3,7 +3,7 @@
     python tools/op_bench.py bfv_mul|ckks_mul|ckks_rot|ckks_hrot|bfv_rot|bfv_hrot [--batch 32] [--reps 10]
                              [--openfhe-primes]
 
-*_hrot: 4 hoisted rotations of the batch (fhe_rotate_hoisted); the rate counts rotations.
+*_hrot: --rot (default 4) hoisted rotations of the batch (fhe_rotate_hoisted); the rate counts rotations.
 
 --openfhe-primes: the CKKS ops on OpenFHE-style primes (q = 1 mod 2N, generic
 Montgomery path) instead of the default q = 1 (mod 2^32) family.
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--openfhe-primes", action="store_true")
+    ap.add_argument("--rot", type=int, default=4, help="Galois elements per hoisted call (*_hrot)")
     args = ap.parse_args()
     import torch
     import herdsman_amd.backend as hb
@@ -42,7 +43,7 @@ def main():
     k = c.fill_uniform(hb.empty(c.key_shape()), seed=3)
     out = hb.empty(shape)
     g = c.galois_elt(1)
-    gs = [c.galois_elt(s_) for s_ in (1, 2, -1, 5)]
+    gs = [c.galois_elt(s_) for s_ in range(1, args.rot + 1)]
     outs = [hb.empty(shape) for _ in gs] if args.op.endswith("hrot") else []
     per = len(gs) if args.op.endswith("hrot") else 1
     fn = {"bfv_mul": lambda: c.mul_relin(a, b, k, out), "ckks_mul": lambda: c.mul_relin(a, b, k, out),
