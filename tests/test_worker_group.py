@@ -167,7 +167,8 @@ def test_gpu_map_task_mul_rotate(wg_run, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("log_n,steps,lvl", [(16, (0, 1, 3), 11), (12, (1, 2), 4)])
+@pytest.mark.parametrize("log_n,steps,lvl", [(16, (0, 1, 3), 11), (12, (1, 2), 4),
+                                             (12, (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10), 4)])
 def test_gpu_map_task_rotsum_hoisted(wg_run, tmp_path, log_n, steps, lvl):
     """ROTSUM: the sum of the input's rotations by the given steps (0 = the input
     itself), the rotations hoisted (fhe_rotate_hoisted_at: one ModUp of c1);
