@@ -286,13 +286,27 @@ __global__ void __launch_bounds__(EW_BLOCK) ks_combine_kernel(const u64 *__restr
 // d_bfv_kscale, so they are the conversion's v_k) as 31-bit column sums, and the
 // combine, per element:  out_b[i] = base_b[i] + (acc_b[i] - sum_k v_k [P/p_k]_{q_i}) P^-1.
 // h = the ModDown table [K][L] ((P/p_k) R mod q_i), K <= 4.
+// several rotations' ModDown in one launch (hoisted BFV rotations of few
+// ciphertexts): poly p of acc is rotation p / rp, ciphertext poly p % rp
+struct BfvRotOut {
+  u32 rp;  // 0: one rotation (the out / base_ginv arguments)
+  u64 *out[FHE_ROT_BATCH];
+  u32 ginv[FHE_ROT_BATCH];
+};
 template <bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) bfv_moddown_kernel(const u64 *__restrict__ acc, const u64 *base, u64 *out,
                                                                const u64 *__restrict__ h, const u64 *pinv,
                                                                const ModInfo *mods, u32 L, u32 K, u32 QP,
-                                                               u32 log_n, u32 add_mask, u32 base_ginv) {
+                                                               u32 log_n, u32 add_mask, u32 base_ginv, BfvRotOut ro) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
-  const u32 p = blockIdx.y / L, i = blockIdx.y % L;  // p = 2 ct + b
+  const u32 p = blockIdx.y / L, i = blockIdx.y % L;  // p = 2 ct + b (of the rotation batch)
+  u32 cp = p;
+  if (ro.rp) {
+    const u32 r = p / ro.rp;
+    cp = p - r * ro.rp;
+    out = ro.out[r];
+    base_ginv = ro.ginv[r];
+  }
   const size_t N = (size_t)1 << log_n;
   const ModInfo m = mods[i];
   const u64 *ap = acc + (size_t)p * QP * N + k;
@@ -307,14 +321,14 @@ __global__ void __launch_bounds__(EW_BLOCK) bfv_moddown_kernel(const u64 *__rest
   }
   const u64 cv = csub63(dot_cols<4, SP>(v, h0, h1, m), m.q);
   u64 ks = csub63(mont_mul<SP>(sub_mod(ap[(size_t)i * N], cv, m.q), pinv[i], m), m.q);
-  const size_t o = ((size_t)p * L + i) * N + k;
+  const size_t o = ((size_t)cp * L + i) * N + k;
   if (add_mask & (1u << (p & 1))) {
     u64 bv;
     if (base_ginv) {
       // the base read through the coefficient automorphism (rotation: sigma_g(c0)
       // is never stored; the map of aut_rows_coef_kernel)
       const u32 n = 1u << log_n, j0 = (u32)(((u64)k * base_ginv) & (2 * n - 1));
-      const u64 *bp = base + ((size_t)p * L + i) * N;
+      const u64 *bp = base + ((size_t)cp * L + i) * N;
       bv = j0 < n ? bp[j0] : (bp[j0 - n] ? m.q - bp[j0 - n] : 0);
     } else {
       bv = base[o];
@@ -953,14 +967,26 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
 
 template <bool SP>
 static int bfv_moddown_impl(fhe_ctx *c, const u64 *acc, const u64 *base, u64 *out, u32 n, u32 add_mask,
-                            u32 base_ginv) {
+                            u32 base_ginv, const RotBatch *rb = nullptr) {
   const u32 L = c->L, per = std::max<u32>(1, kMaxGridY / L);
   const size_t N = c->n, QP = c->L + c->K;
-  for (u32 p0 = 0; p0 < 2 * n; p0 += per) {
-    const u32 np = std::min(per, 2 * n - p0);
+  BfvRotOut ro{};
+  const u32 nr = rb ? rb->nr : 1;
+  if (rb) {
+    // one launch over the batch: acc holds nr rotations of the n ciphertexts
+    if (nr < 1 || nr > FHE_ROT_BATCH || 2 * n * nr > per) return fhe_fail(c, FHE_ERR_INVALID, "rotation batch");
+    ro.rp = 2 * n;
+    for (u32 r = 0; r < nr; ++r) {
+      ro.out[r] = rb->out[r];
+      ro.ginv[r] = galois_inv(rb->g[r], c->log_n);
+    }
+  }
+  for (u32 p0 = 0; p0 < 2 * n * nr; p0 += per) {
+    const u32 np = std::min(per, 2 * n * nr - p0);
     hipLaunchKernelGGL((bfv_moddown_kernel<SP>), dim3(c->n / EW_BLOCK, np * L), dim3(EW_BLOCK), 0, c->stream,
-                       acc + (size_t)p0 * QP * N, base + (size_t)p0 * L * N, out + (size_t)p0 * L * N, c->moddown.h,
-                       c->d_pinv, c->d_mods, L, c->K, (u32)QP, c->log_n, add_mask, base_ginv);
+                       acc + (size_t)p0 * QP * N, base + (rb ? 0 : (size_t)p0 * L * N),
+                       rb ? nullptr : out + (size_t)p0 * L * N, c->moddown.h, c->d_pinv, c->d_mods, L, c->K,
+                       (u32)QP, c->log_n, add_mask, base_ginv, ro);
     int rc = fhe_check(c, hipGetLastError(), "bfv_moddown_kernel");
     if (rc) return rc;
   }
@@ -1129,7 +1155,7 @@ static bool hoisted_gather(const fhe_ctx *c) {
 // per CU; hoisting's common case is one ciphertext and many rotations)
 constexpr u32 ROT_BATCH_CTS = 32;
 static u32 hoisted_rot_batch(const fhe_ctx *c, u32 n) {
-  if (c->params.scheme != FHE_SCHEME_CKKS || !hoisted_gather(c)) return 1;
+  if (!hoisted_gather(c)) return 1;
   return std::max<u32>(1, std::min<u32>(FHE_ROT_BATCH, ROT_BATCH_CTS / std::max<u32>(n, 1)));
 }
 size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n) {
@@ -1166,6 +1192,23 @@ int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois,
     // ModDown reading c0 through the coefficient map
     if ((rc = SP_DISPATCH(c, ks_prep_impl, c, ct + LN, 2 * c->L, w.dc, w.ext, n, w.ndig, c->d_bfv_dscale))) return rc;
     if ((rc = bfv_ks_extend(c, w, n))) return rc;
+    const u32 nrb = hoisted_rot_batch(c, n);
+    if (nrb > 1) {
+      // few ciphertexts: several Galois elements per launch (as CKKS below)
+      u64 *accb = w.conv + (size_t)n * 2 * LN;
+      for (u32 r0 = 0; r0 < n_rot; r0 += nrb) {
+        RotBatch rb{};
+        rb.nr = std::min(nrb, n_rot - r0);
+        for (u32 r = 0; r < rb.nr; ++r) {
+          rb.ksk[r] = gks[r0 + r];
+          rb.out[r] = outs[r0 + r];
+          rb.g[r] = galois[r0 + r];
+        }
+        if ((rc = ntt_inv_ksp_launch(c, accb, w.ext, nullptr, n, w.ndig, 0, true, &rb))) return rc;
+        if ((rc = SP_DISPATCH(c, bfv_moddown_impl, c, accb, ct, nullptr, n, 1u, 0u, &rb))) return rc;
+      }
+      return FHE_OK;
+    }
     for (u32 r = 0; r < n_rot; ++r)
       if ((rc = bfv_ks_finish(c, w, gks[r], ct, outs[r], n, 1u, galois[r], galois_inv(galois[r], c->log_n))))
         return rc;

@@ -166,6 +166,16 @@ def test_bfv_hoisted(hb, log_n, L, K, dnum):
     assert np.array_equal(_run(hb, c, ct, gs, gks), o.rotate_hoisted(ct, gs, np.stack(gks)))
 
 
+def test_bfv_hoisted_rotation_batches(hb):
+    """BFV at C3 parameters, one ciphertext, 10 Galois elements: 8 + 2 per launch."""
+    o = Oracle(SCHEME_BFV, 15, 8, 4, 2, t=65537)
+    c = hb.Context(SCHEME_BFV, 15, 8, 4, 2, t=65537, moduli=o.moduli)
+    ct = o.uniform((1, 2, o.L, o.n), seed=1700)
+    gs = [o.galois_elt(k) for k in (1, 2, 3, 4, 5, -1, -2, -3, -4, -5)]
+    gks = [o.uniform(o.key_shape(), seed=1710 + i) for i in range(len(gs))]
+    assert np.array_equal(_run(hb, c, ct, gs, gks), o.rotate_hoisted(ct, gs, np.stack(gks)))
+
+
 def test_hoisted_chunked_batch(hb):
     """More ciphertexts than one internal pass (kCtChunk = 512): the outputs of
     every chunk land at their own offsets."""
