@@ -411,8 +411,16 @@ static void keyswitch_lvl(const orc_ctx *c, const uint64_t *d, const uint64_t *k
                           uint32_t lvl) {
   keyswitch_lvl_g(c, d, ksk, out, in_ntt, lvl, 0);
 }
+/* n_keys > 1 (double-hoisted rotation sum): the inner products of every key
+ * ksks[r] with sigma_{ext_gs[r]}(ModUp(d)) are summed before ONE ModDown. */
+static void keyswitch_lvl_multi(const orc_ctx *c, const uint64_t *d, uint32_t n_keys, const uint64_t *const *ksks,
+                                const uint32_t *ext_gs, uint64_t *out, int in_ntt, uint32_t lvl);
 static void keyswitch_lvl_g(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, int in_ntt,
                             uint32_t lvl, uint32_t ext_g) {
+  keyswitch_lvl_multi(c, d, 1, &ksk, &ext_g, out, in_ntt, lvl);
+}
+static void keyswitch_lvl_multi(const orc_ctx *c, const uint64_t *d, uint32_t n_keys, const uint64_t *const *ksks,
+                                const uint32_t *ext_gs, uint64_t *out, int in_ntt, uint32_t lvl) {
   const uint32_t n = c->n, L = lvl, K = c->K, QP = L + K, QPk = c->L + K, A = c->alpha;
 #define MI(i) ((i) < L ? (i) : c->L + ((i) - L))
   uint64_t *dc = malloc(sizeof(uint64_t) * L * n);        /* d in coef form */
@@ -437,25 +445,28 @@ static void keyswitch_lvl_g(const orc_ctx *c, const uint64_t *d, const uint64_t 
     conv_tab_init(T, sq, hi - lo, dq, nd);
     conv_apply(T, sp, dp, n);
     for (uint32_t k = 0; k < nd; ++k) ntt_fwd_limb(&c->m[MI(didx[k])], ext + (size_t)didx[k] * n, n);
-    if (ext_g) {  /* hoisted rotation: sigma_g on the digit's extension (a slot permutation per limb) */
-      uint64_t *tmp = malloc(sizeof(uint64_t) * QP * n);
-      orc_automorph_ntt(c, ext, tmp, ext_g, 1, QP);
-      memcpy(ext, tmp, sizeof(uint64_t) * QP * n);
-      free(tmp);
-    }
-    /* inner product with key digit j (its rows of Q_lvl u P) */
-    for (uint32_t b = 0; b < 2; ++b) {
-      const uint64_t *kj = ksk + ((size_t)(j * 2 + b) * QPk) * n;
-      uint64_t *ab = acc + (size_t)b * QP * n;
-      for (uint32_t i = 0; i < QP; ++i) {
-        const uint64_t q = c->m[MI(i)].q;
-        const uint64_t *kr = kj + (size_t)MI(i) * n;
-        for (uint32_t k = 0; k < n; ++k) {
-          size_t o = (size_t)i * n + k;
-          ab[o] = addmod(ab[o], mulmod(ext[o], kr[k], q), q);
+    uint64_t *tmp = malloc(sizeof(uint64_t) * QP * n);
+    for (uint32_t r = 0; r < n_keys; ++r) {
+      const uint64_t *e = ext;
+      if (ext_gs[r]) {  /* hoisted rotation: sigma_g on the digit's extension (a slot permutation per limb) */
+        orc_automorph_ntt(c, ext, tmp, ext_gs[r], 1, QP);
+        e = tmp;
+      }
+      /* inner product with key digit j (its rows of Q_lvl u P) */
+      for (uint32_t b = 0; b < 2; ++b) {
+        const uint64_t *kj = ksks[r] + ((size_t)(j * 2 + b) * QPk) * n;
+        uint64_t *ab = acc + (size_t)b * QP * n;
+        for (uint32_t i = 0; i < QP; ++i) {
+          const uint64_t q = c->m[MI(i)].q;
+          const uint64_t *kr = kj + (size_t)MI(i) * n;
+          for (uint32_t k = 0; k < n; ++k) {
+            size_t o = (size_t)i * n + k;
+            ab[o] = addmod(ab[o], mulmod(e[o], kr[k], q), q);
+          }
         }
       }
     }
+    free(tmp);
   }
   /* ModDown: (acc_Q - Conv_{P->Q}(acc_P)) * P^-1 */
   uint64_t pq[MAXM], qq[MAXM];
@@ -894,6 +905,33 @@ void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, co
 void orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                            const uint64_t *gks, uint64_t *outs, uint32_t n_ct, uint32_t lvl) {
   rotate_hoisted_lvl(c, ct, n_rot, galois, gks, outs, n_ct, lvl);
+}
+
+/* Double-hoisted rotation sum (Bossuat et al.'s hoisted ModDown): out = sum_r
+ * rot_{g_r}(ct), the key-switch inner products of every element summed in
+ * Q u P before ONE ModDown, plus sum_r sigma_{g_r}(c0).  Decrypts to the sum of
+ * the rotated messages; the bits differ from summing hoisted rotations by the
+ * ModDown rounding.  out [n_ct][2][lvl][N]. */
+void orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                               const uint64_t *gks, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+  const size_t L = lvl, N = c->n, CT = 2 * L * N, KW = (size_t)c->dnum * 2 * (c->L + c->K) * N;
+  const int ckks = c->scheme == ORC_SCHEME_CKKS;
+  const uint64_t **ks_r = malloc(sizeof(uint64_t *) * (n_rot ? n_rot : 1));
+  for (uint32_t r = 0; r < n_rot; ++r) ks_r[r] = gks + r * KW;
+#pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
+  for (long i = 0; i < (long)n_ct; ++i) {
+    uint64_t *o = out + i * CT;
+    uint64_t *ks = malloc(sizeof(uint64_t) * CT), *rot = malloc(sizeof(uint64_t) * L * N);
+    keyswitch_lvl_multi(c, ct + i * CT + L * N, n_rot, ks_r, galois, ks, ckks, (uint32_t)L);
+    memcpy(o, ks, sizeof(uint64_t) * CT);
+    for (uint32_t r = 0; r < n_rot; ++r) {
+      if (ckks) orc_automorph_ntt(c, ct + i * CT, rot, galois[r], 1, (uint32_t)L);
+      else orc_automorph_coef(c, ct + i * CT, rot, galois[r], 1, 0, (uint32_t)L);
+      orc_add(c, o, rot, o, 1, 0, (uint32_t)L);
+    }
+    free(ks); free(rot);
+  }
+  free(ks_r);
 }
 
 /* ------------------------------------------------- CKKS levels (rescale) */

@@ -66,6 +66,7 @@ def lib():
         "orc_rescale": (None, [vp, _u64p, _u64p, u32, u32]),
         "orc_rotate_hoisted": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32]),
         "orc_rotate_hoisted_at": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32, u32]),
+        "orc_rotate_sum_hoisted_at": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32, u32]),
         "orc_fill_uniform": (None, [vp, _u64p, u32, u32, u32, u64]),
         "orc_sample_ternary": (None, [vp, u64, _i64p]),
         "orc_sample_cbd": (None, [vp, u64, _i64p]),
@@ -172,6 +173,15 @@ class Oracle:
         gs = np.ascontiguousarray(galois, dtype=np.uint32)
         out = np.zeros((len(gs),) + ct.shape, dtype=np.uint64)
         self.lib.orc_rotate_hoisted(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), out, ct.shape[0])
+        return out
+
+    def rotate_sum_hoisted(self, ct, galois, gks, lvl=None):
+        """double-hoisted sum of rotations: ct [n][2][lvl][N] -> [n][2][lvl][N]"""
+        ct = np.ascontiguousarray(ct)
+        gs = np.ascontiguousarray(galois, dtype=np.uint32)
+        out = np.zeros(ct.shape, dtype=np.uint64)
+        self.lib.orc_rotate_sum_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), out, ct.shape[0],
+                                           ct.shape[2] if lvl is None else lvl)
         return out
 
     def rotate_hoisted_at(self, ct, galois, gks, lvl):

@@ -172,3 +172,40 @@ def test_bfv_hoisted_rotations_decrypt_exactly(mult):
     for r, g in enumerate(gs):
         assert dec(outs[r, 0]) == [v % t for v in automorph_int(m1, g)]
         assert dec(outs[r, 1]) == [v % t for v in automorph_int(want_prod, g)]
+
+
+def test_rotation_sum_double_hoisted_decrypts():
+    """Double-hoisted rotation sum (one ModDown for all the Galois elements):
+    BFV decrypts exactly to sum_r rot_r(m) mod t, CKKS within the noise bound,
+    at the full level and (CKKS) at a reduced one."""
+    t = 65537
+    o = Oracle(SCHEME_BFV, 10, 4, 2, 2, t=t)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    Qp = math.prod(Q)
+    s, s_qp = _keys(o)
+    rng = random.Random(21)
+    m1 = [rng.randrange(t) for _ in range(o.n)]
+    c1 = o.encrypt(to_rns([(Qp // t) * x for x in m1], Q), s_qp, 909)
+    gs = [o.galois_elt(k) for k in (1, 2, -3)]
+    gks = np.stack([o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=60 + i) for i, g in enumerate(gs)])
+    out = o.rotate_sum_hoisted(c1[None], gs, gks)[0]
+    v = crt_centered(o.decrypt(out, s_qp), Q)
+    got = [((t * x + Qp // 2) // Qp) % t for x in v]
+    want = [sum(col) % t for col in zip(*[automorph_int(m1, g) for g in gs])]
+    assert got == want
+
+    o = Oracle(SCHEME_CKKS, 10, 4, 2, 2)
+    s, s_qp = _keys(o)
+    delta = 1 << 40
+    u = [rng.randint(-100, 100) for _ in range(o.n)]
+    for lvl in (4, 3):
+        Ql = [int(q) for q in o.moduli[:lvl]]
+        ct = o.encrypt(to_rns([delta * x for x in u], [int(q) for q in o.moduli[:o.L]]), s_qp, 919)
+        ct = np.ascontiguousarray(ct[:, :lvl])
+        gks = np.stack([o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=70 + i) for i, g in enumerate(gs)])
+        out = o.rotate_sum_hoisted(ct[None], gs, gks)[0]
+        qs = o.moduli[:lvl].astype(object)[:, None]
+        m = ((out[0].astype(object) + out[1].astype(object) * s_qp[:lvl].astype(object)) % qs).astype(np.uint64)
+        dec = crt_centered(o.ntt_inv(m[None])[0], Ql)
+        want = [delta * sum(col) for col in zip(*[automorph_int(u, g) for g in gs])]
+        assert max(abs(a - b) for a, b in zip(dec, want)) < 2 ** 30, lvl
