@@ -80,6 +80,8 @@ SIGNATURES = {
     "fhe_galois_elt": (C.c_int, [_vp, _i32, C.POINTER(_u32)]),
     "fhe_rotate_hoisted": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32]),
     "fhe_rotate_hoisted_at": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32]),
+    "fhe_rotate_sum_hoisted": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32]),
+    "fhe_rotate_sum_hoisted_at": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32]),
     "fhe_add_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
     "fhe_sub_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
     "fhe_mul_relin_at": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _u32, _u32]),
@@ -320,6 +322,25 @@ class Context:
         """CKKS: outs[r] = rotation of ct by galois[r] with key gks[r], one ModUp of c1 for all."""
         n = self._ct_batch(ct, *outs)
         return self._hoisted(self.lib.fhe_rotate_hoisted, ct, galois, gks, outs, n)
+
+    def _rot_sum(self, fn, ct, galois, gks, out, n, *extra):
+        if len(galois) != len(gks) or not galois:
+            raise FheBackendError("rotation sum: galois and gks must have one (non-zero) length")
+        for k in gks:
+            self._key(k)
+        ga = np.ascontiguousarray(galois, dtype=np.uint32)
+        ka = (C.c_uint64 * len(gks))(*[_ptr(k) for k in gks])
+        self._ck(fn(self.h, _ptr(ct), len(ga), ga.ctypes.data, C.addressof(ka), _ptr(out), n, *extra), fn.__name__)
+        return out
+
+    def rotate_sum_hoisted(self, ct, galois, gks, out):
+        """out = sum_r rot_{galois[r]}(ct), one ModDown for all the elements (double hoisting)."""
+        n = self._ct_batch(ct, out)
+        return self._rot_sum(self.lib.fhe_rotate_sum_hoisted, ct, galois, gks, out, n)
+
+    def rotate_sum_hoisted_at(self, ct, galois, gks, out, level: int):
+        n = self._ct_level(level, ct, out)
+        return self._rot_sum(self.lib.fhe_rotate_sum_hoisted_at, ct, galois, gks, out, n, level)
 
     # ---- CKKS levels: ciphertexts [n][2][level][N] over the first `level` Q primes
     def _ct_level(self, level: int, *cts):

@@ -230,6 +230,10 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
 int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois, const u64 *const *gks,
                         u64 *const *outs, u32 n);
 size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n);
+// double-hoisted rotation sum: out [n][2][L][N] = sum_r rot_{g_r}(ct), one ModDown
+int rotate_sum_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois, const u64 *const *gks, u64 *out,
+                            u32 n);
+size_t rotate_sum_ws_bytes(const fhe_ctx *c, u32 n);
 // CKKS rescale of n ciphertexts of level m + 1 (on `up`, the context of level
 // m + 1) to level m (on `lo`, the context of level m); ct must not overlap out
 int rescale_impl(fhe_ctx *up, fhe_ctx *lo, const u64 *ct, u64 *out, u32 n);

@@ -497,7 +497,7 @@ int fhe_reserve(fhe_ctx *c, uint32_t max_batch) {
   max_batch = std::min(max_batch, kCtChunk);  // ops run in passes of at most kCtChunk ciphertexts
   size_t need = (size_t)sizeof(u64) * c->n * max_batch * 2 * c->L;  // rotate / mul scratch
   if (c->K) need += keyswitch_ws_bytes(c, max_batch);
-  if (c->K) need = std::max(need, rotate_hoisted_ws_bytes(c, max_batch));
+  if (c->K) need = std::max({need, rotate_hoisted_ws_bytes(c, max_batch), rotate_sum_ws_bytes(c, max_batch)});
   if (c->nB) need = std::max(need, bfv_mul_ws_bytes(c, max_batch));
   void *p;
   return ctx_workspace(c, need, &p);
@@ -726,6 +726,27 @@ int fhe_rotate_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uin
   return FHE_OK;
 }
 
+int fhe_rotate_sum_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                           const uint64_t *const *gks, uint64_t *out, uint32_t n_ct) {
+  if (!c) return FHE_ERR_INVALID;
+  if (c->K == 0) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "context has no special primes (K = 0)");
+  if (!n_ct) return FHE_OK;
+  if (!n_rot || !galois || !gks || !ct || !out) return fhe_fail(c, FHE_ERR_INVALID, "null array or no rotations");
+  DeviceBind bind(c);
+  for (uint32_t r = 0; r < n_rot; ++r) {
+    const uint32_t g = galois[r];
+    if ((g & 1) == 0 || g >= 2 * c->n) return fhe_fail(c, FHE_ERR_INVALID, "galois element must be odd and < 2N");
+    if (!gks[r]) return fhe_fail(c, FHE_ERR_INVALID, "null key");
+  }
+  const size_t cw = (size_t)2 * c->L * c->n;
+  for (uint32_t c0 = 0; c0 < n_ct; c0 += kCtChunk) {
+    const uint32_t m = std::min(kCtChunk, n_ct - c0);
+    int rc = rotate_sum_hoisted_impl(c, ct + c0 * cw, n_rot, galois, gks, out + c0 * cw, m);
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
 // ---- CKKS levels: the op of the level-m view, its error reported on c
 static int at_level(fhe_ctx *c, uint32_t level, fhe_ctx **v) {
   if (!c) return FHE_ERR_INVALID;
@@ -774,6 +795,14 @@ int fhe_rotate_hoisted_at(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const 
   DeviceBind bind(c);
   int rc = at_level(c, level, &v);
   return rc ? rc : from_view(c, v, fhe_rotate_hoisted(v, ct, n_rot, galois, gks, outs, n_ct));
+}
+
+int fhe_rotate_sum_hoisted_at(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                              const uint64_t *const *gks, uint64_t *out, uint32_t n_ct, uint32_t level) {
+  fhe_ctx *v;
+  DeviceBind bind(c);
+  int rc = at_level(c, level, &v);
+  return rc ? rc : from_view(c, v, fhe_rotate_sum_hoisted(v, ct, n_rot, galois, gks, out, n_ct));
 }
 
 int fhe_rescale(fhe_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t level) {

@@ -338,6 +338,78 @@ __global__ void __launch_bounds__(EW_BLOCK) bfv_moddown_kernel(const u64 *__rest
   out[o] = ks;
 }
 
+// Double-hoisted rotation sum (orc_rotate_sum_hoisted_at): the key-switch
+// inner products of up to ROT_SUM_MAX Galois elements over every limb of Q u P,
+//   acc_b[i][k] (+)= sum_r sum_j ext_j[i][sigma_{g_r}(k)] ksk_r[j][b][row(i)][k] R^-1,
+// ext in the NTT domain (times R, lazy below 8q on special moduli).  One thread
+// per (coefficient, limb, ciphertext); acc canonical.
+#define ROT_SUM_MAX 16
+struct RotSumArgs {
+  u32 nr;
+  const u64 *ksk[ROT_SUM_MAX];
+  u32 g[ROT_SUM_MAX];  // Galois elements (NTT gathers); the coefficient map takes g^-1 (aut_sum_kernel)
+};
+__device__ __forceinline__ u32 ntt_aut_src(u32 k, u32 g, u32 log_n) {
+  const u32 mask = (2u << log_n) - 1;
+  const u32 e = 2 * (__brev(k) >> (32 - log_n)) + 1;
+  const u32 e2 = (u32)(((u64)e * g) & mask);
+  return __brev((e2 - 1) >> 1) >> (32 - log_n);
+}
+template <bool SP>
+__global__ void __launch_bounds__(EW_BLOCK) rot_sum_inner_kernel(const u64 *__restrict__ ext, u64 *__restrict__ acc,
+                                                                 RotSumArgs ra, const ModInfo *mods, u32 L, u32 QP,
+                                                                 u32 ndig, u32 kQP, u32 kshift, u32 log_n,
+                                                                 u32 accumulate) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x, i = blockIdx.y, ct = blockIdx.z;
+  const size_t N = (size_t)1 << log_n;
+  const ModInfo m = mods[i];  // the context's own index space (a level view: Q_m then P)
+  const u64 *e = ext + ((size_t)ct * ndig * QP + i) * N;
+  const size_t row = i < L ? i : i + kshift;  // the full-level key row
+  const u64 q2 = 2 * m.q;
+  u64 s0 = 0, s1 = 0;
+  for (u32 r = 0; r < ra.nr; ++r) {
+    const u32 src = ntt_aut_src(k, ra.g[r], log_n);
+    const u64 *kp = ra.ksk[r] + row * N + k;
+    for (u32 j = 0; j < ndig; ++j) {
+      const u64 x = e[(size_t)j * QP * N + src];
+      s0 = csub(s0 + mont_mul<SP>(x, kp[(size_t)(2 * j) * kQP * N], m), q2);  // < 2q
+      s1 = csub(s1 + mont_mul<SP>(x, kp[(size_t)(2 * j + 1) * kQP * N], m), q2);
+    }
+  }
+  s0 = csub(s0, m.q);
+  s1 = csub(s1, m.q);
+  u64 *o0 = acc + ((size_t)ct * 2 * QP + i) * N + k, *o1 = o0 + (size_t)QP * N;
+  if (accumulate) {
+    s0 = add_mod(s0, *o0, m.q);
+    s1 = add_mod(s1, *o1, m.q);
+  }
+  *o0 = s0;
+  *o1 = s1;
+}
+// base[ct][0][i] (+)= sum_r sigma_{g_r}(c0[ct][i]): NTT-domain gathers (CKKS) or
+// the signed coefficient map with g^-1 (BFV)
+__global__ void __launch_bounds__(EW_BLOCK) rot_sum_base_kernel(const u64 *__restrict__ ct, u64 *__restrict__ base,
+                                                                RotSumArgs ra, const ModInfo *mods, u32 L, u32 log_n,
+                                                                u32 coef, u32 accumulate) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x, i = blockIdx.y, c = blockIdx.z;
+  const size_t N = (size_t)1 << log_n;
+  const u64 q = mods[i].q;
+  const u64 *c0 = ct + ((size_t)c * 2 * L + i) * N;
+  u64 s = 0;
+  for (u32 r = 0; r < ra.nr; ++r) {
+    u64 v;
+    if (coef) {
+      const u32 n = 1u << log_n, j0 = (u32)(((u64)k * ra.g[r]) & (2 * n - 1));
+      v = j0 < n ? c0[j0] : (c0[j0 - n] ? q - c0[j0 - n] : 0);
+    } else {
+      v = c0[ntt_aut_src(k, ra.g[r], log_n)];
+    }
+    s = add_mod(s, v, q);
+  }
+  u64 *o = base + ((size_t)c * 2 * L + i) * N + k;
+  *o = accumulate ? add_mod(s, *o, q) : s;
+}
+
 // Rotation input: (c0, c1) -> sigma_g, fused with the key-switch preparation:
 //   base[ct][0] = sigma(c0); dc[ct] = sigma(c1); ext[ct][own] = sigma(c1) * R.
 // NTT domain (CKKS): slot permutation; coefficient domain (BFV): signed gather.
@@ -1256,6 +1328,72 @@ int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois,
     if (rc) return rc;
   }
   return FHE_OK;
+}
+
+size_t rotate_sum_ws_bytes(const fhe_ctx *c, u32 n) {
+  return keyswitch_ws_bytes(c, n) + sizeof(u64) * c->n * (size_t)n * 2 * c->L;
+}
+
+// Double-hoisted rotation sum (orc_rotate_sum_hoisted_at; Bossuat et al.'s
+// hoisted ModDown): c1 extended once, the inner products of every Galois
+// element summed over Q u P (rot_sum_inner_kernel, sigma_g as a gather), ONE
+// ModDown, plus sum_r sigma_{g_r}(c0).  out may alias ct (ct is read before the
+// ModDown writes out).
+int rotate_sum_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois, const u64 *const *gks, u64 *out,
+                            u32 n) {
+  const size_t LN = (size_t)c->L * c->n;
+  const u32 L = c->L, K = c->K, QP = L + K;
+  const bool ckks = c->params.scheme == FHE_SCHEME_CKKS;
+  void *ws;
+  int rc = ctx_workspace(c, rotate_sum_ws_bytes(c, n), &ws);
+  if (rc) return rc;
+  const KsWs w = ks_layout(c, n, (u64 *)ws);
+  u64 *base = w.conv + (size_t)n * 2 * LN;  // [n][2][L][N], poly 0 = sum_r sigma_r(c0)
+  if (ckks && c->log_n > 14) {
+    if ((rc = ntt_inv_automorph_launch(c, ct, 1u, nullptr, w.dc, w.ext, n, w.ndig))) return rc;
+  } else if ((rc = SP_DISPATCH(c, ks_prep_impl, c, ct + LN, 2 * L, w.dc, w.ext, n, w.ndig, nullptr))) {
+    return rc;
+  }
+  if ((rc = ks_extend(c, w, n, ckks, ckks && c->log_n > 14))) return rc;
+  for (u32 r0 = 0; r0 < n_rot; r0 += ROT_SUM_MAX) {
+    RotSumArgs ra{}, rb{};
+    ra.nr = rb.nr = std::min<u32>(ROT_SUM_MAX, n_rot - r0);
+    for (u32 r = 0; r < ra.nr; ++r) {
+      ra.ksk[r] = gks[r0 + r];
+      ra.g[r] = galois[r0 + r] & ((2u << c->log_n) - 1);
+      rb.g[r] = ckks ? ra.g[r] : galois_inv(galois[r0 + r], c->log_n);
+    }
+    for (u32 c0 = 0; c0 < n; c0 += kMaxGridY) {
+      const u32 nc = std::min<u32>(kMaxGridY, n - c0);
+      if (c->special)
+        hipLaunchKernelGGL((rot_sum_inner_kernel<true>), dim3(c->n / EW_BLOCK, QP, nc), dim3(EW_BLOCK), 0, c->stream,
+                           w.ext + (size_t)c0 * w.ndig * QP * c->n, w.acc + (size_t)c0 * 2 * QP * c->n, ra, c->d_mods,
+                           L, QP, w.ndig, ctx_key_qp(c), c->key_pshift, c->log_n, r0 > 0 ? 1u : 0u);
+      else
+        hipLaunchKernelGGL((rot_sum_inner_kernel<false>), dim3(c->n / EW_BLOCK, QP, nc), dim3(EW_BLOCK), 0, c->stream,
+                           w.ext + (size_t)c0 * w.ndig * QP * c->n, w.acc + (size_t)c0 * 2 * QP * c->n, ra, c->d_mods,
+                           L, QP, w.ndig, ctx_key_qp(c), c->key_pshift, c->log_n, r0 > 0 ? 1u : 0u);
+      if ((rc = fhe_check(c, hipGetLastError(), "rot_sum_inner_kernel"))) return rc;
+      hipLaunchKernelGGL(rot_sum_base_kernel, dim3(c->n / EW_BLOCK, L, nc), dim3(EW_BLOCK), 0, c->stream,
+                         ct + (size_t)c0 * 2 * LN, base + (size_t)c0 * 2 * LN, rb, c->d_mods, L, c->log_n,
+                         ckks ? 0u : 1u, r0 > 0 ? 1u : 0u);
+      if ((rc = fhe_check(c, hipGetLastError(), "rot_sum_base_kernel"))) return rc;
+    }
+  }
+  // ONE ModDown of the summed accumulator (keyswitch_run's finish without the
+  // fused inner products): out = base + (acc_Q - Conv(acc_P)) P^-1
+  u64 *acc = w.acc, *conv = w.conv;
+  const size_t N = c->n;
+  if (ckks && c->fuse_moddown) {
+    if ((rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale))) return rc;
+    return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, 1u, &c->moddown);
+  }
+  if ((rc = ntt_launch(c, LimbMap{acc, QP, ckks ? K : QP, ckks ? L : 0, QP, 0, 0, 2 * n}, true,
+                       ckks && c->fold_ninv)))
+    return rc;
+  if ((rc = conv_launch(c, c->moddown, acc + (size_t)L * N, QP, conv, L, 2 * n))) return rc;
+  if (ckks) return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, 1u);
+  return SP_DISPATCH(c, combine_impl, c, acc, conv, base, out, n, 1u);
 }
 
 // ------------------------------------------------------------ CKKS rescale

@@ -154,6 +154,14 @@ int fhe_rotate(fhe_ctx *ctx, const uint64_t *ct, uint32_t galois_elt, const uint
  * coefficient domain, as the other ciphertext ops. */
 int fhe_rotate_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
                        const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct);
+/* double-hoisted rotation sum: out [n_ct][2][L][N] = sum_r rot_{galois_elts[r]}(ct)
+ * with the key-switch inner products of all n_rot >= 1 elements summed in
+ * Q u P before ONE ModDown (the hoisted-ModDown baby-step sum of linear
+ * transforms).  Decrypts to the sum of the rotated messages; the bits differ
+ * from adding fhe_rotate_hoisted's outputs by the ModDown rounding (oracle
+ * orc_rotate_sum_hoisted_at).  galois_elts, gks: HOST arrays; out may alias ct. */
+int fhe_rotate_sum_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
+                           const uint64_t *const *gks, uint64_t *out, uint32_t n_ct);
 /* 5^steps mod 2N (steps may be negative); conjugation is 2N-1 */
 int fhe_galois_elt(const fhe_ctx *ctx, int32_t steps, uint32_t *out);
 
@@ -177,6 +185,8 @@ int fhe_keyswitch_at(fhe_ctx *ctx, const uint64_t *d, const uint64_t *ksk, uint6
                      uint32_t level);
 int fhe_rotate_hoisted_at(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
                           const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct, uint32_t level);
+int fhe_rotate_sum_hoisted_at(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
+                              const uint64_t *const *gks, uint64_t *out, uint32_t n_ct, uint32_t level);
 /* CKKS rescale, level -> level - 1 (2 <= level <= L): out [n_ct][2][level-1][N]
  * = round(ct / q_{level-1}) -- OpenFHE DCRTPoly::DropLastElementAndScale /
  * SEAL divide_and_round_q_last_ntt (the dropped limb lifted centrally).

@@ -186,3 +186,39 @@ def test_hoisted_chunked_batch(hb):
     gks = [o.uniform(o.key_shape(), seed=1401 + i) for i in range(len(gs))]
     c.reserve(520)
     assert np.array_equal(_run(hb, c, ct, gs, gks), o.rotate_hoisted(ct, gs, np.stack(gks)))
+
+
+# ---- double-hoisted rotation sum (fhe_rotate_sum_hoisted[_at]): one ModDown
+@pytest.mark.parametrize("scheme,log_n,L,K,dnum,n_ct,steps", [
+    (SCHEME_CKKS, 16, 12, 4, 3, 2, (1, 2, -1, 5, -7)),
+    (SCHEME_CKKS, 12, 5, 2, 3, 3, (1, 2, 3)),
+    (SCHEME_CKKS, 12, 4, 2, 2, 1, tuple(range(1, 19))),  # two chunks of the 16-element kernel
+    (SCHEME_BFV, 15, 8, 4, 2, 2, (1, -2, 3)),
+    (SCHEME_BFV, 12, 5, 2, 3, 1, (2, 4)),
+])
+def test_rotation_sum_double_hoisted(hb, scheme, log_n, L, K, dnum, n_ct, steps):
+    t = 65537 if scheme == SCHEME_BFV else 0
+    o = Oracle(scheme, log_n, L, K, dnum, t=t)
+    c = hb.Context(scheme, log_n, L, K, dnum, t=t, moduli=o.moduli)
+    ct = o.uniform((n_ct, 2, L, o.n), seed=1800 + log_n + len(steps))
+    gs = [o.galois_elt(k) for k in steps]
+    gks = [o.uniform(o.key_shape(), seed=1820 + i) for i in range(len(gs))]
+    want = o.rotate_sum_hoisted(ct, gs, np.stack(gks))
+    d_gk = [hb.to_device(k) for k in gks]
+    out = hb.empty(ct.shape)
+    c.rotate_sum_hoisted(hb.to_device(ct), gs, d_gk, out)
+    assert np.array_equal(hb.to_host(out), want)
+    io = hb.to_device(ct)  # in place
+    c.rotate_sum_hoisted(io, gs, d_gk, io)
+    assert np.array_equal(hb.to_host(io), want)
+
+
+def test_rotation_sum_double_hoisted_at_level(hb, metric):
+    o, c = metric
+    lvl = 7
+    ct = o.uniform((1, 2, lvl, o.n), seed=1900)
+    gs = [o.galois_elt(k) for k in (1, 3, -2)]
+    gks = [o.uniform(o.key_shape(), seed=1910 + i) for i in range(len(gs))]
+    out = hb.empty(ct.shape)
+    c.rotate_sum_hoisted_at(hb.to_device(ct), gs, [hb.to_device(k) for k in gks], out, lvl)
+    assert np.array_equal(hb.to_host(out), o.rotate_sum_hoisted(ct, gs, np.stack(gks), lvl))
