@@ -845,9 +845,9 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
         break;
       }
       case Op::ROTSUM: {
-        // sum of hoisted rotations: fhe_rotate_hoisted_at over the steps in the
-        // mask, at most 8 Galois elements per call (the output buffers are reused
-        // from call to call), accumulated with fhe_add_at (bit 0: the input itself)
+        // sum of rotations by the steps in the mask, double-hoisted: one ModUp
+        // of c1 and ONE ModDown for all of them (fhe_rotate_sum_hoisted_at); bit 0
+        // adds the input itself
         if (stack.empty()) throw std::runtime_error("circuit stack underflow");
         const uint32_t mask = (uint32_t)ins.arg;
         if (mask == 0 || (mask >> 31)) throw std::runtime_error("rotsum step mask must be in [1, 2^31)");
@@ -860,38 +860,12 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
           gks.push_back(galois_key(s, ks, k, &g).p);
           gs.push_back(g);
         }
-        const size_t T = gs.size(), G = std::min<size_t>(T, 8);
-        if (T == 0) break;  // mask 1: the input itself
+        if (gs.empty()) break;  // mask 1: the input itself
         const uint64_t *top = stack.back().buf.p;
-        std::vector<ArenaBuf> outs;
-        std::vector<uint64_t *> outp;
-        for (size_t r = 0; r < G; ++r) {
-          outs.emplace_back(*ls.arena, s.ct_words(m) * n);
-          outp.push_back(outs.back().p);
-        }
-        const auto hoisted = [&](size_t c0, size_t cnt) {
-          ck(s.ctx, fhe_rotate_hoisted_at(s.ctx, top, (uint32_t)cnt, gs.data() + c0, gks.data() + c0, outp.data(),
-                                          (uint32_t)n, m), "rotate_hoisted");
-        };
-        if (T == 1 && !(mask & 1)) {
-          hoisted(0, 1);
-          stack.back() = StackCt{std::move(outs[0]), m};
-          break;
-        }
         StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
-        const uint64_t *acc = (mask & 1) ? top : nullptr;
-        for (size_t c0 = 0; c0 < T; c0 += G) {
-          const size_t cnt = std::min(G, T - c0);
-          hoisted(c0, cnt);
-          for (size_t r = 0; r < cnt; ++r) {
-            if (!acc) {  // the first term; the second one starts the sum in o
-              acc = outp[r];
-              continue;
-            }
-            ck(s.ctx, fhe_add_at(s.ctx, acc, outp[r], o.buf.p, (uint32_t)n, m), "rotsum add");
-            acc = o.buf.p;
-          }
-        }
+        ck(s.ctx, fhe_rotate_sum_hoisted_at(s.ctx, top, (uint32_t)gs.size(), gs.data(), gks.data(), o.buf.p,
+                                            (uint32_t)n, m), "rotate_sum_hoisted");
+        if (mask & 1) ck(s.ctx, fhe_add_at(s.ctx, o.buf.p, top, o.buf.p, (uint32_t)n, m), "rotsum add");
         stack.back() = std::move(o);
         break;
       }

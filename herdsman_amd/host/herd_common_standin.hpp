@@ -56,8 +56,9 @@ struct CryptoKeyPtr {
 // CKKS operands may sit at different levels: binary ops run at the lower one
 // (the other operand's extra limbs dropped), RESCALE drops one level.
 // ROTSUM replaces the top with sum_{i in arg} rot_i(top), arg a bit mask
-// of step counts 0..30 (bit 0: the ciphertext itself), the rotations hoisted
-// (one ModUp of c1 for all of them: a baby-step block of a linear transform).
+// of step counts 0..30 (bit 0: the ciphertext itself), double-hoisted (one
+// ModUp of c1 and one ModDown for all of them: a baby-step block of a linear
+// transform).
 enum class CtOp : uint32_t { PUSH_INPUT = 0, ADD = 1, SUB = 2, MUL_RELIN = 3, ROTATE = 4, RESCALE = 5, ROTSUM = 6 };
 struct CircuitInstr {
   CtOp op;

@@ -171,7 +171,7 @@ def test_gpu_map_task_mul_rotate(wg_run, tmp_path):
                                              (12, (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10), 4)])
 def test_gpu_map_task_rotsum_hoisted(wg_run, tmp_path, log_n, steps, lvl):
     """ROTSUM: the sum of the input's rotations by the given steps (0 = the input
-    itself), the rotations hoisted (fhe_rotate_hoisted_at: one ModUp of c1);
+    itself), double-hoisted (fhe_rotate_sum_hoisted_at: one ModUp, one ModDown);
     at N=2^16 on level-11 rows (the fused gather path at a reduced level), at
     N=2^12 after a product (the generic path)."""
     from oracle_ffi import SCHEME_CKKS
@@ -192,7 +192,7 @@ def test_gpu_map_task_rotsum_hoisted(wg_run, tmp_path, log_n, steps, lvl):
     assert r.returncode == 0, r.stdout + r.stderr
     got = np.stack([parse_row(o, p, level=lvl) for p in read_partition(os.path.join(storage, "sr", "fb", "0"))])
     x = a if log_n == 16 else o.mul_relin_at(a, b, rlk, lvl)
-    terms = list(o.rotate_hoisted_at(x, gs, np.stack(gks), lvl)) + ([x] if 0 in steps else [])
+    terms = [o.rotate_sum_hoisted(x, gs, np.stack(gks), lvl)] + ([x] if 0 in steps else [])
     qs = o.moduli[:lvl].astype(object)[None, None, :, None]
     want = sum(t.astype(object) for t in terms) % qs
     assert np.array_equal(got, want.astype(np.uint64))
@@ -200,7 +200,7 @@ def test_gpu_map_task_rotsum_hoisted(wg_run, tmp_path, log_n, steps, lvl):
 
 @pytest.mark.gpu
 def test_gpu_map_task_rotsum_bfv(wg_run, tmp_path):
-    """ROTSUM on BFV rows (C3 parameters): hoisted rotations in coefficient form."""
+    """ROTSUM on BFV rows (C3 parameters): the double-hoisted sum in coefficient form."""
     from oracle_ffi import SCHEME_BFV
     o, storage, keys = _setup(tmp_path, SCHEME_BFV, 15, 8, 4, 2, t=65537)
     rows = 2
@@ -215,7 +215,7 @@ def test_gpu_map_task_rotsum_bfv(wg_run, tmp_path):
                         "in0", "rotsum:0,2,5"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     got = np.stack([parse_row(o, p) for p in read_partition(os.path.join(storage, "sb", "fb", "1"))])
-    terms = list(o.rotate_hoisted(a, gs, np.stack(gks))) + [a]
+    terms = [o.rotate_sum_hoisted(a, gs, np.stack(gks)), a]
     qs = o.moduli[:o.L].astype(object)[None, None, :, None]
     want = sum(t.astype(object) for t in terms) % qs
     assert np.array_equal(got, want.astype(np.uint64))
