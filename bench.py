@@ -562,7 +562,8 @@ def _timed(fn, reps, stream):
 def secondary_configs(hb, ctx, gk, a, b, out, dev, stream, B, reps):
     """Per-GPU throughput of the other BASELINE.json configs (same synthetic-data rules):
     C4 CKKS rotate + hybrid KS at the metric parameters (B ciphertexts per call) and
-    4 hoisted rotations of the same batch (fhe_rotate_hoisted, one ModUp of c1),
+    4 hoisted rotations of the same batch (fhe_rotate_hoisted, one ModUp of c1) and the
+    double-hoisted sum of 16 rotations (fhe_rotate_sum_hoisted, one ModUp and one ModDown),
     C3 BFV mul+relin at N=2^15 L=8 (BEHZ), C2 forward+inverse NTT at N=2^14 L=4, and
     the metric op on OpenFHE-style primes (q = 1 mod 2N, generic Montgomery path)
     next to the same single-context call on the default primes."""
@@ -580,6 +581,10 @@ def secondary_configs(hb, ctx, gk, a, b, out, dev, stream, B, reps):
     t = _timed(lambda: ctx.rotate_hoisted(ct, gs, [gk] * len(gs), hos), reps, stream)
     res["C4_ckks_rotate_hoisted4_rot_per_s"] = round(len(gs) * B / t, 1)
     del hos
+    # double-hoisted sum of 16 rotations (one ModUp, one ModDown): rotations per second summed
+    g16 = [ctx.galois_elt(s_) for s_ in range(1, 17)]
+    t = _timed(lambda: ctx.rotate_sum_hoisted(ct, g16, [gk] * len(g16), o), reps, stream)
+    res["C4_ckks_rotate_sum16_rot_per_s"] = round(len(g16) * B / t, 1)
     t = _timed(lambda: ctx.mul_relin(ct, b[:B], gk, o), reps, stream)
     res["C5_mul_relin_1ctx_per_s"] = round(B / t, 1)
     # the CKKS multiply as a circuit runs it: mul+relin then rescale (12 -> 11 limbs),
