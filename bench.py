@@ -736,6 +736,11 @@ def cpu_baseline_child(args):
     done, dt = timed(lambda: o.rotate_hoisted(a, gs, k4), len(gs) * threads, 3.0)
     sec["C4_ckks_rotate_hoisted4_rot_per_s"] = round(done / dt, 3)
     del k4
+    g16 = [o.galois_elt(s_) for s_ in range(1, 17)]
+    k16 = np.stack([k] * len(g16))
+    done, dt = timed(lambda: o.rotate_sum_hoisted(a, g16, k16), len(g16) * threads, 3.0)
+    sec["C4_ckks_rotate_sum16_rot_per_s"] = round(done / dt, 3)
+    del k16
     del a, b, k
     o3 = Oracle(SCHEME_BFV, 15, 8, 4, 2, t=65537)
     a3 = o3.uniform((threads, 2, 8, 1 << 15), seed=31)
