@@ -215,11 +215,14 @@ class Params:
 
 
 # ------------------------------------------------------- hybrid keyswitch
-def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = None, ext_g: int = 0):
+def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = None, ext_g: int = 0, multi=None):
     """Hybrid key switching at level lvl (default L).  d: lvl limbs (NTT form if
     ntt_form).  ksk[j][b][i] limb i of Q u P of the FULL-level key (NTT form);
     at a reduced level the digits partition the lvl active limbs by alpha and
-    only the key rows of Q_lvl u P are used.  Returns (ks0, ks1), each lvl limbs."""
+    only the key rows of Q_lvl u P are used.  Returns (ks0, ks1), each lvl limbs.
+    multi = [(ksk_r, g_r), ...] (double-hoisted rotation sum): the inner products
+    of every key with sigma_{g_r}(ext) are summed before the one ModDown."""
+    keys = multi if multi is not None else [(ksk, ext_g)]
     L, K = (p.L if lvl is None else lvl), p.K
     mi = list(range(L)) + [p.L + k for k in range(K)]  # level space -> modulus / key row
     QP = list(range(L + K))
@@ -240,16 +243,17 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = Non
             ext[i] = dn[i]
         for i, c in zip(others, conv_n):
             ext[i] = c
-        if ext_g:  # hoisted rotation: sigma_g applied to the digit's extension
-            ext = {i: automorph_ntt(e, ext_g) for i, e in ext.items()}
-        for b in range(2):
-            for i in QP:
-                q = p.moduli[mi[i]]
-                kb = ksk[j][b][mi[i]]
-                e = ext[i]
-                row = acc[b][i]
-                for k in range(p.n):
-                    row[k] = (row[k] + e[k] * kb[k]) % q
+        for kr, g in keys:
+            # hoisted rotation: sigma_g applied to the digit's extension
+            ex = {i: automorph_ntt(e, g) for i, e in ext.items()} if g else ext
+            for b in range(2):
+                for i in QP:
+                    q = p.moduli[mi[i]]
+                    kb = kr[j][b][mi[i]]
+                    e = ex[i]
+                    row = acc[b][i]
+                    for k in range(p.n):
+                        row[k] = (row[k] + e[k] * kb[k]) % q
     Pprod = math.prod(p.P)
     Qs = p.moduli[:L]
     out = []
@@ -270,6 +274,21 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = Non
             res.append([(accQ[i][k] - conv[i][k]) * pinv % q for k in range(p.n)])
         out.append(res)
     return out
+
+
+def rotate_sum_hoisted(p: Params, ct, gs, gks):
+    """Double-hoisted rotation sum: sum_r rot_{g_r}(ct) with the inner products of
+    every key summed before ONE ModDown, plus sum_r sigma_{g_r}(c0)."""
+    ckks = p.scheme == "ckks"
+    ks0, ks1 = keyswitch(p, ct[1], None, ckks, None, 0, list(zip(gks, gs)))
+    c0 = ks0
+    for g in gs:
+        if ckks:
+            r0 = [automorph_ntt(x, g) for x in ct[0]]
+        else:
+            r0 = [automorph_coef(x, g, p.moduli[i]) for i, x in enumerate(ct[0])]
+        c0 = [[(x + y) % p.moduli[i] for x, y in zip(c0[i], r0[i])] for i in range(p.L)]
+    return [c0, ks1]
 
 
 def ckks_mul_relin_at(p: Params, a, b, rlk, lvl: int):

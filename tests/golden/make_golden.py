@@ -120,6 +120,31 @@ def gen_bfv_hoisted(rng):
              galois=np.array(gs, dtype=np.uint32), gks=arr(gks), out=arr(out))
 
 
+def gen_rotation_sums(rng):
+    """Double-hoisted rotation sums (one ModDown for all the elements): CKKS N=1024
+    L=5 and BFV N=1024 L=4, three elements each with their own keys."""
+    out = {}
+    log_n, n = 10, 1 << 10
+    Q = M.gen_primes(60, log_n, 5)
+    P = M.gen_primes(61, log_n, 2, exclude=Q)
+    p = M.Params(log_n, 5, 2, 2, Q + P)
+    ct = [rand_limbs(rng, Q, n) for _ in range(2)]
+    gs = [M.galois_elt(log_n, 1), M.galois_elt(log_n, 3), 2 * n - 1]
+    gks = [[[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(2)] for _ in gs]
+    out["ckks"] = dict(moduli=arr(Q + P), ct=arr(ct), galois=np.array(gs, dtype=np.uint32), gks=arr(gks),
+                       out=arr(M.rotate_sum_hoisted(p, ct, gs, gks)))
+    Qb = M.gen_primes(60, log_n, 4)
+    Pb = M.gen_primes(61, log_n, 2, exclude=Qb)
+    Bsk = M.gen_primes(61, log_n, 5, exclude=Qb + Pb)
+    pb = M.Params(log_n, 4, 2, 2, Qb + Pb + Bsk, "bfv", 65537)
+    ctb = [rand_limbs(rng, Qb, n) for _ in range(2)]
+    gksb = [[[rand_limbs(rng, Qb + Pb, n) for _ in range(2)] for _ in range(2)] for _ in gs]
+    out["bfv"] = dict(moduli=arr(Qb + Pb + Bsk), ct=arr(ctb), galois=np.array(gs, dtype=np.uint32), gks=arr(gksb),
+                      out=arr(M.rotate_sum_hoisted(pb, ctb, gs, gksb)))
+    np.savez(os.path.join(HERE, "rotation_sum_n1024.npz"), log_n=np.uint32(log_n),
+             **{f"{s}_{k}": v for s, d in out.items() for k, v in d.items()})
+
+
 def gen_bfv_hps(rng):
     """BFV mul+relin by HPS (oracle/bigint_model.py bfv_mul_relin_hps, which also
     checks each scaled tensor output against round(t d / Q) on integers)."""
@@ -196,6 +221,7 @@ def main():
     gen_bfv_hps(random.Random(0x485053))
     gen_ckks_hoisted(random.Random(0x484F4953))
     gen_bfv_hoisted(random.Random(0x42484F49))
+    gen_rotation_sums(random.Random(0x52534D))
     print("golden vectors written to", HERE)
 
 
@@ -208,5 +234,7 @@ if __name__ == "__main__":
         gen_ckks_hoisted(random.Random(0x484F4953))
     elif sys.argv[1:] == ["hoisted_bfv"]:
         gen_bfv_hoisted(random.Random(0x42484F49))
+    elif sys.argv[1:] == ["rotation_sums"]:
+        gen_rotation_sums(random.Random(0x52534D))
     else:
         main()

@@ -222,3 +222,16 @@ def test_rotation_sum_double_hoisted_at_level(hb, metric):
     out = hb.empty(ct.shape)
     c.rotate_sum_hoisted_at(hb.to_device(ct), gs, [hb.to_device(k) for k in gks], out, lvl)
     assert np.array_equal(hb.to_host(out), o.rotate_sum_hoisted(ct, gs, np.stack(gks), lvl))
+
+
+@pytest.mark.parametrize("scheme", ["ckks", "bfv"])
+def test_rotation_sum_golden(hb, scheme):
+    g = np.load(os.path.join(GOLD, "rotation_sum_n1024.npz"))
+    if scheme == "ckks":
+        c = hb.Context(SCHEME_CKKS, int(g["log_n"]), 5, 2, 2, moduli=g["ckks_moduli"])
+    else:
+        c = hb.Context(SCHEME_BFV, int(g["log_n"]), 4, 2, 2, t=65537, moduli=g["bfv_moduli"])
+    out = hb.empty((1,) + g[f"{scheme}_ct"].shape)
+    c.rotate_sum_hoisted(hb.to_device(g[f"{scheme}_ct"][None]), [int(x) for x in g[f"{scheme}_galois"]],
+                         [hb.to_device(k) for k in g[f"{scheme}_gks"]], out)
+    assert np.array_equal(hb.to_host(out)[0], g[f"{scheme}_out"])

@@ -145,3 +145,15 @@ def test_bfv_hoisted_rotations_golden():
                moduli=g["moduli"])
     out = o.rotate_hoisted(g["ct"][None], g["galois"], g["gks"])
     assert np.array_equal(out[:, 0], g["out"])
+
+
+@pytest.mark.parametrize("scheme", ["ckks", "bfv"])
+def test_rotation_sum_golden(scheme):
+    g = load("rotation_sum_n1024.npz")
+    mods = g[f"{scheme}_moduli"]
+    if scheme == "ckks":
+        o = Oracle(SCHEME_CKKS, int(g["log_n"]), 5, 2, 2, moduli=mods)
+    else:
+        o = Oracle(SCHEME_BFV, int(g["log_n"]), 4, 2, 2, t=65537, moduli=mods)
+    out = o.rotate_sum_hoisted(g[f"{scheme}_ct"][None], g[f"{scheme}_galois"], g[f"{scheme}_gks"])
+    assert np.array_equal(out[0], g[f"{scheme}_out"])
