@@ -5,7 +5,7 @@ sweep draws (log_n, L, K, dnum, scheme, BFV technique, prime family) from a
 fixed seed so that partial last digits, alpha not dividing L, K < alpha,
 one-pass and two-pass sizes, both lazy-schedule classes and both BFV
 multiplication techniques meet every op: mul+relin, rotate, keyswitch,
-hoisted rotations, and for CKKS rescale, a level-reduced mul+relin and
+hoisted rotations, the double-hoisted rotation sum, and for CKKS rescale, a level-reduced mul+relin and
 level-reduced hoisted rotations.
 """
 import random
@@ -77,6 +77,8 @@ def test_sweep(hb, i, scheme, log_n, L, K, dnum, generic, mult):
     want = o.rotate_hoisted(a, gs, np.stack([k, k]))
     for r in range(len(gs)):
         assert np.array_equal(hb.to_host(outs[r]), want[r]), ("hoisted", r)
+    c.rotate_sum_hoisted(da, gs, [dk, dk], out)
+    assert np.array_equal(hb.to_host(out), o.rotate_sum_hoisted(a, gs, np.stack([k, k]))), "rotation sum"
     if scheme != SCHEME_CKKS:
         return
     if L >= 2:
