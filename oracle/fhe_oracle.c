@@ -413,14 +413,19 @@ static void keyswitch_lvl(const orc_ctx *c, const uint64_t *d, const uint64_t *k
 }
 /* n_keys > 1 (double-hoisted rotation sum): the inner products of every key
  * ksks[r] with sigma_{ext_gs[r]}(ModUp(d)) are summed before ONE ModDown. */
+/* pts (optional, hoisted linear transform): key r's inner product is weighted by
+ * the plaintext pts[r] ([L+K][N] NTT form, the rows of Q_lvl u P used like the
+ * key's) before the sum. */
 static void keyswitch_lvl_multi(const orc_ctx *c, const uint64_t *d, uint32_t n_keys, const uint64_t *const *ksks,
-                                const uint32_t *ext_gs, uint64_t *out, int in_ntt, uint32_t lvl);
+                                const uint32_t *ext_gs, const uint64_t *const *pts, uint64_t *out, int in_ntt,
+                                uint32_t lvl);
 static void keyswitch_lvl_g(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, int in_ntt,
                             uint32_t lvl, uint32_t ext_g) {
-  keyswitch_lvl_multi(c, d, 1, &ksk, &ext_g, out, in_ntt, lvl);
+  keyswitch_lvl_multi(c, d, 1, &ksk, &ext_g, NULL, out, in_ntt, lvl);
 }
 static void keyswitch_lvl_multi(const orc_ctx *c, const uint64_t *d, uint32_t n_keys, const uint64_t *const *ksks,
-                                const uint32_t *ext_gs, uint64_t *out, int in_ntt, uint32_t lvl) {
+                                const uint32_t *ext_gs, const uint64_t *const *pts, uint64_t *out, int in_ntt,
+                                uint32_t lvl) {
   const uint32_t n = c->n, L = lvl, K = c->K, QP = L + K, QPk = c->L + K, A = c->alpha;
 #define MI(i) ((i) < L ? (i) : c->L + ((i) - L))
   uint64_t *dc = malloc(sizeof(uint64_t) * L * n);        /* d in coef form */
@@ -459,9 +464,12 @@ static void keyswitch_lvl_multi(const orc_ctx *c, const uint64_t *d, uint32_t n_
         for (uint32_t i = 0; i < QP; ++i) {
           const uint64_t q = c->m[MI(i)].q;
           const uint64_t *kr = kj + (size_t)MI(i) * n;
+          const uint64_t *pr = pts ? pts[r] + (size_t)MI(i) * n : NULL;
           for (uint32_t k = 0; k < n; ++k) {
             size_t o = (size_t)i * n + k;
-            ab[o] = addmod(ab[o], mulmod(e[o], kr[k], q), q);
+            uint64_t v = mulmod(e[o], kr[k], q);
+            if (pr) v = mulmod(v, pr[k] % q, q);
+            ab[o] = addmod(ab[o], v, q);
           }
         }
       }
@@ -922,7 +930,7 @@ void orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_
   for (long i = 0; i < (long)n_ct; ++i) {
     uint64_t *o = out + i * CT;
     uint64_t *ks = malloc(sizeof(uint64_t) * CT), *rot = malloc(sizeof(uint64_t) * L * N);
-    keyswitch_lvl_multi(c, ct + i * CT + L * N, n_rot, ks_r, galois, ks, ckks, (uint32_t)L);
+    keyswitch_lvl_multi(c, ct + i * CT + L * N, n_rot, ks_r, galois, NULL, ks, ckks, (uint32_t)L);
     memcpy(o, ks, sizeof(uint64_t) * CT);
     for (uint32_t r = 0; r < n_rot; ++r) {
       if (ckks) orc_automorph_ntt(c, ct + i * CT, rot, galois[r], 1, (uint32_t)L);
@@ -932,6 +940,38 @@ void orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_
     free(ks); free(rot);
   }
   free(ks_r);
+}
+
+/* Hoisted linear transform (CKKS): out = sum_r pts[r] (.) rot_{g_r}(ct), the
+ * plaintext-weighted inner products of every element summed in Q u P before
+ * ONE ModDown, plus sum_r pts[r] (.) sigma_{g_r}(c0).  pts [n_rot][L+K][N] in
+ * the NTT domain (full-level rows; a level uses rows 0..lvl-1 and L..L+K-1). */
+void orc_linear_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                           const uint64_t *gks, const uint64_t *pts, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+  const size_t L = lvl, N = c->n, CT = 2 * L * N, KW = (size_t)c->dnum * 2 * (c->L + c->K) * N;
+  const size_t PW = (size_t)(c->L + c->K) * N;
+  const uint64_t **ks_r = malloc(sizeof(uint64_t *) * (n_rot ? n_rot : 1));
+  const uint64_t **pt_r = malloc(sizeof(uint64_t *) * (n_rot ? n_rot : 1));
+  for (uint32_t r = 0; r < n_rot; ++r) { ks_r[r] = gks + r * KW; pt_r[r] = pts + r * PW; }
+#pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
+  for (long i = 0; i < (long)n_ct; ++i) {
+    uint64_t *o = out + i * CT;
+    uint64_t *ks = malloc(sizeof(uint64_t) * CT), *rot = malloc(sizeof(uint64_t) * L * N);
+    keyswitch_lvl_multi(c, ct + i * CT + L * N, n_rot, ks_r, galois, pt_r, ks, 1, (uint32_t)L);
+    memcpy(o, ks, sizeof(uint64_t) * CT);
+    for (uint32_t r = 0; r < n_rot; ++r) {
+      orc_automorph_ntt(c, ct + i * CT, rot, galois[r], 1, (uint32_t)L);
+      for (uint32_t li = 0; li < L; ++li) {
+        const uint64_t q = c->m[li].q;
+        for (size_t k = 0; k < N; ++k) {
+          const size_t x = li * N + k;
+          o[x] = addmod(o[x], mulmod(rot[x], pt_r[r][li * N + k] % q, q), q);
+        }
+      }
+    }
+    free(ks); free(rot);
+  }
+  free(ks_r); free(pt_r);
 }
 
 /* ------------------------------------------------- CKKS levels (rescale) */

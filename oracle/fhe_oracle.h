@@ -100,6 +100,9 @@ void orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot,
 /* double-hoisted rotation sum: out [n_ct][2][lvl][N] = sum_r rot_{g_r}(ct), one ModDown */
 void orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                                const uint64_t *gks, uint64_t *out, uint32_t n_ct, uint32_t lvl);
+/* hoisted linear transform (CKKS): out = sum_r pts[r] (.) rot_{g_r}(ct), one ModDown */
+void orc_linear_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                           const uint64_t *gks, const uint64_t *pts, uint64_t *out, uint32_t n_ct, uint32_t lvl);
 
 /* ---- CKKS levels: ciphertexts [n_ct][2][lvl][N] with the first lvl Q primes
  * (1 <= lvl <= L).  Key switching at level lvl uses the full-level key's rows

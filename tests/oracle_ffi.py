@@ -67,6 +67,7 @@ def lib():
         "orc_rotate_hoisted": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32]),
         "orc_rotate_hoisted_at": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32, u32]),
         "orc_rotate_sum_hoisted_at": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32, u32]),
+        "orc_linear_hoisted_at": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, _u64p, u32, u32]),
         "orc_fill_uniform": (None, [vp, _u64p, u32, u32, u32, u64]),
         "orc_sample_ternary": (None, [vp, u64, _i64p]),
         "orc_sample_cbd": (None, [vp, u64, _i64p]),
@@ -182,6 +183,15 @@ class Oracle:
         out = np.zeros(ct.shape, dtype=np.uint64)
         self.lib.orc_rotate_sum_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), out, ct.shape[0],
                                            ct.shape[2] if lvl is None else lvl)
+        return out
+
+    def linear_hoisted(self, ct, galois, gks, pts, lvl=None):
+        """hoisted linear transform: sum_r pts[r] (.) rot_r(ct); pts [r][L+K][N] NTT form"""
+        ct = np.ascontiguousarray(ct)
+        gs = np.ascontiguousarray(galois, dtype=np.uint32)
+        out = np.zeros(ct.shape, dtype=np.uint64)
+        self.lib.orc_linear_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), np.ascontiguousarray(pts),
+                                       out, ct.shape[0], ct.shape[2] if lvl is None else lvl)
         return out
 
     def rotate_hoisted_at(self, ct, galois, gks, lvl):

@@ -209,3 +209,32 @@ def test_rotation_sum_double_hoisted_decrypts():
         dec = crt_centered(o.ntt_inv(m[None])[0], Ql)
         want = [delta * sum(col) for col in zip(*[automorph_int(u, g) for g in gs])]
         assert max(abs(a - b) for a, b in zip(dec, want)) < 2 ** 30, lvl
+
+
+def test_linear_transform_hoisted_decrypts():
+    """Hoisted linear transform (CKKS): sum_r w_r * rot_r(m) with plaintexts w_r
+    (small integer polynomials, NTT form over Q u P), one ModDown for the whole
+    sum: decrypts to Delta * sum_r w_r * rot_r(u) within the noise bound."""
+    o = Oracle(SCHEME_CKKS, 10, 4, 2, 2)
+    Q = [int(q) for q in o.moduli[:o.L]]
+    s, s_qp = _keys(o)
+    rng = random.Random(31)
+    delta = 1 << 40
+    u = [rng.randint(-50, 50) for _ in range(o.n)]
+    ct = o.encrypt(to_rns([delta * x for x in u], Q), s_qp, 929)
+    gs = [o.galois_elt(k) for k in (1, 2, -1)]
+    gks = np.stack([o.switch_key(o.automorph_ntt(s_qp, g), s_qp, seed=80 + i) for i, g in enumerate(gs)])
+    ws = []
+    for _ in gs:
+        w = [0] * o.n
+        for _ in range(4):
+            w[rng.randrange(o.n)] = rng.randint(-2, 2)
+        ws.append(w)
+    pts = np.stack([o.signed_to_rns(w, 0, o.L + o.K, ntt=True) for w in ws])
+    out = o.linear_hoisted(ct[None], gs, gks, pts)[0]
+    dec = crt_centered(o.decrypt(out, s_qp), Q)
+    want = [0] * o.n
+    for g, w in zip(gs, ws):
+        for i, v in enumerate(negacyclic_int(w, automorph_int(u, g))):
+            want[i] += delta * v
+    assert max(abs(a - b) for a, b in zip(dec, want)) < 2 ** 34
