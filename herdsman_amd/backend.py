@@ -82,6 +82,8 @@ SIGNATURES = {
     "fhe_rotate_hoisted_at": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32]),
     "fhe_rotate_sum_hoisted": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32]),
     "fhe_rotate_sum_hoisted_at": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _u32, _u32]),
+    "fhe_linear_hoisted": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]),
+    "fhe_linear_hoisted_at": (C.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _u32]),
     "fhe_add_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
     "fhe_sub_at": (C.c_int, [_vp, _vp, _vp, _vp, _u32, _u32]),
     "fhe_mul_relin_at": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _u32, _u32]),
@@ -332,6 +334,31 @@ class Context:
         ka = (C.c_uint64 * len(gks))(*[_ptr(k) for k in gks])
         self._ck(fn(self.h, _ptr(ct), len(ga), ga.ctypes.data, C.addressof(ka), _ptr(out), n, *extra), fn.__name__)
         return out
+
+    def _linear(self, fn, ct, galois, gks, pts, out, n, *extra):
+        if not (len(galois) == len(gks) == len(pts)) or not galois:
+            raise FheBackendError("linear transform: galois, gks and pts must have one (non-zero) length")
+        for k in gks:
+            self._key(k)
+        for p in pts:
+            if tuple(p.shape) != (self.L + self.K, self.n):
+                raise FheBackendError(f"plaintext shape {tuple(p.shape)}, expected {(self.L + self.K, self.n)}")
+            self._on_device(p)
+        ga = np.ascontiguousarray(galois, dtype=np.uint32)
+        ka = (C.c_uint64 * len(gks))(*[_ptr(k) for k in gks])
+        pa = (C.c_uint64 * len(pts))(*[_ptr(p) for p in pts])
+        self._ck(fn(self.h, _ptr(ct), len(ga), ga.ctypes.data, C.addressof(ka), C.addressof(pa), _ptr(out), n,
+                    *extra), fn.__name__)
+        return out
+
+    def linear_hoisted(self, ct, galois, gks, pts, out):
+        """CKKS: out = sum_r pts[r] (.) rot_{galois[r]}(ct), one ModDown (pts [L+K][N] NTT form)."""
+        n = self._ct_batch(ct, out)
+        return self._linear(self.lib.fhe_linear_hoisted, ct, galois, gks, pts, out, n)
+
+    def linear_hoisted_at(self, ct, galois, gks, pts, out, level: int):
+        n = self._ct_level(level, ct, out)
+        return self._linear(self.lib.fhe_linear_hoisted_at, ct, galois, gks, pts, out, n, level)
 
     def rotate_sum_hoisted(self, ct, galois, gks, out):
         """out = sum_r rot_{galois[r]}(ct), one ModDown for all the elements (double hoisting)."""

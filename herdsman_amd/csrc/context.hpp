@@ -231,8 +231,9 @@ int rotate_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois,
                         u64 *const *outs, u32 n);
 size_t rotate_hoisted_ws_bytes(const fhe_ctx *c, u32 n);
 // double-hoisted rotation sum: out [n][2][L][N] = sum_r rot_{g_r}(ct), one ModDown
+// (pts: the hoisted linear transform sum_r pts[r] (.) rot_r(ct), CKKS; null: plain sum)
 int rotate_sum_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois, const u64 *const *gks, u64 *out,
-                            u32 n);
+                            u32 n, const u64 *const *pts = nullptr);
 size_t rotate_sum_ws_bytes(const fhe_ctx *c, u32 n);
 // CKKS rescale of n ciphertexts of level m + 1 (on `up`, the context of level
 // m + 1) to level m (on `lo`, the context of level m); ct must not overlap out

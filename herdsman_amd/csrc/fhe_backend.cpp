@@ -726,8 +726,23 @@ int fhe_rotate_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uin
   return FHE_OK;
 }
 
+static int rot_sum(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois, const uint64_t *const *gks,
+                   const uint64_t *const *pts, uint64_t *out, uint32_t n_ct);
 int fhe_rotate_sum_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                            const uint64_t *const *gks, uint64_t *out, uint32_t n_ct) {
+  return rot_sum(c, ct, n_rot, galois, gks, nullptr, out, n_ct);
+}
+int fhe_linear_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                       const uint64_t *const *gks, const uint64_t *const *pts, uint64_t *out, uint32_t n_ct) {
+  if (!c) return FHE_ERR_INVALID;
+  if (c->params.scheme != FHE_SCHEME_CKKS) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "hoisted linear transforms are CKKS only");
+  if (n_ct && n_rot && !pts) return fhe_fail(c, FHE_ERR_INVALID, "null plaintext array");
+  for (uint32_t r = 0; n_ct && r < n_rot; ++r)
+    if (!pts[r]) return fhe_fail(c, FHE_ERR_INVALID, "null plaintext");
+  return rot_sum(c, ct, n_rot, galois, gks, pts, out, n_ct);
+}
+static int rot_sum(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois, const uint64_t *const *gks,
+                   const uint64_t *const *pts, uint64_t *out, uint32_t n_ct) {
   if (!c) return FHE_ERR_INVALID;
   if (c->K == 0) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "context has no special primes (K = 0)");
   if (!n_ct) return FHE_OK;
@@ -741,7 +756,7 @@ int fhe_rotate_sum_hoisted(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const
   const size_t cw = (size_t)2 * c->L * c->n;
   for (uint32_t c0 = 0; c0 < n_ct; c0 += kCtChunk) {
     const uint32_t m = std::min(kCtChunk, n_ct - c0);
-    int rc = rotate_sum_hoisted_impl(c, ct + c0 * cw, n_rot, galois, gks, out + c0 * cw, m);
+    int rc = rotate_sum_hoisted_impl(c, ct + c0 * cw, n_rot, galois, gks, out + c0 * cw, m, pts);
     if (rc) return rc;
   }
   return FHE_OK;
@@ -803,6 +818,15 @@ int fhe_rotate_sum_hoisted_at(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, co
   DeviceBind bind(c);
   int rc = at_level(c, level, &v);
   return rc ? rc : from_view(c, v, fhe_rotate_sum_hoisted(v, ct, n_rot, galois, gks, out, n_ct));
+}
+
+int fhe_linear_hoisted_at(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                          const uint64_t *const *gks, const uint64_t *const *pts, uint64_t *out, uint32_t n_ct,
+                          uint32_t level) {
+  fhe_ctx *v;
+  DeviceBind bind(c);
+  int rc = at_level(c, level, &v);
+  return rc ? rc : from_view(c, v, fhe_linear_hoisted(v, ct, n_rot, galois, gks, pts, out, n_ct));
 }
 
 int fhe_rescale(fhe_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t level) {

@@ -347,6 +347,7 @@ __global__ void __launch_bounds__(EW_BLOCK) bfv_moddown_kernel(const u64 *__rest
 struct RotSumArgs {
   u32 nr;
   const u64 *ksk[ROT_SUM_MAX];
+  const u64 *pt[ROT_SUM_MAX];  // hoisted linear transform: element r's plaintext ([L+K][N] NTT), or null
   u32 g[ROT_SUM_MAX];  // Galois elements (NTT gathers); the coefficient map takes g^-1 (aut_sum_kernel)
 };
 __device__ __forceinline__ u32 ntt_aut_src(u32 k, u32 g, u32 log_n) {
@@ -370,11 +371,19 @@ __global__ void __launch_bounds__(EW_BLOCK) rot_sum_inner_kernel(const u64 *__re
   for (u32 r = 0; r < ra.nr; ++r) {
     const u32 src = ntt_aut_src(k, ra.g[r], log_n);
     const u64 *kp = ra.ksk[r] + row * N + k;
+    u64 t0 = 0, t1 = 0;
     for (u32 j = 0; j < ndig; ++j) {
       const u64 x = e[(size_t)j * QP * N + src];
-      s0 = csub(s0 + mont_mul<SP>(x, kp[(size_t)(2 * j) * kQP * N], m), q2);  // < 2q
-      s1 = csub(s1 + mont_mul<SP>(x, kp[(size_t)(2 * j + 1) * kQP * N], m), q2);
+      t0 = csub(t0 + mont_mul<SP>(x, kp[(size_t)(2 * j) * kQP * N], m), q2);  // < 2q
+      t1 = csub(t1 + mont_mul<SP>(x, kp[(size_t)(2 * j + 1) * kQP * N], m), q2);
     }
+    if (ra.pt[r]) {  // times the plaintext: w = pt R, so mont_mul(t, w) = t pt
+      const u64 w = csub(mont_mul<SP>(ra.pt[r][row * N + k], m.r2, m), m.q);
+      t0 = mont_mul<SP>(t0, w, m);
+      t1 = mont_mul<SP>(t1, w, m);
+    }
+    s0 = csub(s0 + t0, q2);
+    s1 = csub(s1 + t1, q2);
   }
   s0 = csub(s0, m.q);
   s1 = csub(s1, m.q);
@@ -388,12 +397,14 @@ __global__ void __launch_bounds__(EW_BLOCK) rot_sum_inner_kernel(const u64 *__re
 }
 // base[ct][0][i] (+)= sum_r sigma_{g_r}(c0[ct][i]): NTT-domain gathers (CKKS) or
 // the signed coefficient map with g^-1 (BFV)
+template <bool SP>
 __global__ void __launch_bounds__(EW_BLOCK) rot_sum_base_kernel(const u64 *__restrict__ ct, u64 *__restrict__ base,
                                                                 RotSumArgs ra, const ModInfo *mods, u32 L, u32 log_n,
                                                                 u32 coef, u32 accumulate) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x, i = blockIdx.y, c = blockIdx.z;
   const size_t N = (size_t)1 << log_n;
-  const u64 q = mods[i].q;
+  const ModInfo m = mods[i];
+  const u64 q = m.q;
   const u64 *c0 = ct + ((size_t)c * 2 * L + i) * N;
   u64 s = 0;
   for (u32 r = 0; r < ra.nr; ++r) {
@@ -403,6 +414,10 @@ __global__ void __launch_bounds__(EW_BLOCK) rot_sum_base_kernel(const u64 *__res
       v = j0 < n ? c0[j0] : (c0[j0 - n] ? q - c0[j0 - n] : 0);
     } else {
       v = c0[ntt_aut_src(k, ra.g[r], log_n)];
+    }
+    if (ra.pt[r]) {  // NTT domain (CKKS): times the plaintext's Q row i
+      const u64 w = csub(mont_mul<SP>(ra.pt[r][(size_t)i * N + k], m.r2, m), q);
+      v = csub(mont_mul<SP>(v, w, m), q);
     }
     s = add_mod(s, v, q);
   }
@@ -1340,7 +1355,7 @@ size_t rotate_sum_ws_bytes(const fhe_ctx *c, u32 n) {
 // ModDown, plus sum_r sigma_{g_r}(c0).  out may alias ct (ct is read before the
 // ModDown writes out).
 int rotate_sum_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *galois, const u64 *const *gks, u64 *out,
-                            u32 n) {
+                            u32 n, const u64 *const *pts) {
   const size_t LN = (size_t)c->L * c->n;
   const u32 L = c->L, K = c->K, QP = L + K;
   const bool ckks = c->params.scheme == FHE_SCHEME_CKKS;
@@ -1360,6 +1375,7 @@ int rotate_sum_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *gal
     ra.nr = rb.nr = std::min<u32>(ROT_SUM_MAX, n_rot - r0);
     for (u32 r = 0; r < ra.nr; ++r) {
       ra.ksk[r] = gks[r0 + r];
+      ra.pt[r] = rb.pt[r] = pts ? pts[r0 + r] : nullptr;
       ra.g[r] = galois[r0 + r] & ((2u << c->log_n) - 1);
       rb.g[r] = ckks ? ra.g[r] : galois_inv(galois[r0 + r], c->log_n);
     }
@@ -1374,9 +1390,14 @@ int rotate_sum_hoisted_impl(fhe_ctx *c, const u64 *ct, u32 n_rot, const u32 *gal
                            w.ext + (size_t)c0 * w.ndig * QP * c->n, w.acc + (size_t)c0 * 2 * QP * c->n, ra, c->d_mods,
                            L, QP, w.ndig, ctx_key_qp(c), c->key_pshift, c->log_n, r0 > 0 ? 1u : 0u);
       if ((rc = fhe_check(c, hipGetLastError(), "rot_sum_inner_kernel"))) return rc;
-      hipLaunchKernelGGL(rot_sum_base_kernel, dim3(c->n / EW_BLOCK, L, nc), dim3(EW_BLOCK), 0, c->stream,
-                         ct + (size_t)c0 * 2 * LN, base + (size_t)c0 * 2 * LN, rb, c->d_mods, L, c->log_n,
-                         ckks ? 0u : 1u, r0 > 0 ? 1u : 0u);
+      if (c->special)
+        hipLaunchKernelGGL((rot_sum_base_kernel<true>), dim3(c->n / EW_BLOCK, L, nc), dim3(EW_BLOCK), 0, c->stream,
+                           ct + (size_t)c0 * 2 * LN, base + (size_t)c0 * 2 * LN, rb, c->d_mods, L, c->log_n,
+                           ckks ? 0u : 1u, r0 > 0 ? 1u : 0u);
+      else
+        hipLaunchKernelGGL((rot_sum_base_kernel<false>), dim3(c->n / EW_BLOCK, L, nc), dim3(EW_BLOCK), 0, c->stream,
+                           ct + (size_t)c0 * 2 * LN, base + (size_t)c0 * 2 * LN, rb, c->d_mods, L, c->log_n,
+                           ckks ? 0u : 1u, r0 > 0 ? 1u : 0u);
       if ((rc = fhe_check(c, hipGetLastError(), "rot_sum_base_kernel"))) return rc;
     }
   }

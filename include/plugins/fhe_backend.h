@@ -162,6 +162,13 @@ int fhe_rotate_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const u
  * orc_rotate_sum_hoisted_at).  galois_elts, gks: HOST arrays; out may alias ct. */
 int fhe_rotate_sum_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
                            const uint64_t *const *gks, uint64_t *out, uint32_t n_ct);
+/* hoisted linear transform (CKKS; the baby-step block of a matrix-vector
+ * product): out = sum_r pts[r] (.) rot_{galois_elts[r]}(ct), the plaintext-
+ * weighted inner products summed in Q u P before ONE ModDown.  pts: HOST array
+ * of n_rot device plaintexts [L+K][N] in the NTT domain (full-level rows, used
+ * like the keys' at a reduced level); oracle orc_linear_hoisted_at. */
+int fhe_linear_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
+                       const uint64_t *const *gks, const uint64_t *const *pts, uint64_t *out, uint32_t n_ct);
 /* 5^steps mod 2N (steps may be negative); conjugation is 2N-1 */
 int fhe_galois_elt(const fhe_ctx *ctx, int32_t steps, uint32_t *out);
 
@@ -187,6 +194,9 @@ int fhe_rotate_hoisted_at(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, cons
                           const uint64_t *const *gks, uint64_t *const *outs, uint32_t n_ct, uint32_t level);
 int fhe_rotate_sum_hoisted_at(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
                               const uint64_t *const *gks, uint64_t *out, uint32_t n_ct, uint32_t level);
+int fhe_linear_hoisted_at(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
+                          const uint64_t *const *gks, const uint64_t *const *pts, uint64_t *out, uint32_t n_ct,
+                          uint32_t level);
 /* CKKS rescale, level -> level - 1 (2 <= level <= L): out [n_ct][2][level-1][N]
  * = round(ct / q_{level-1}) -- OpenFHE DCRTPoly::DropLastElementAndScale /
  * SEAL divide_and_round_q_last_ntt (the dropped limb lifted centrally).

@@ -235,3 +235,45 @@ def test_rotation_sum_golden(hb, scheme):
     c.rotate_sum_hoisted(hb.to_device(g[f"{scheme}_ct"][None]), [int(x) for x in g[f"{scheme}_galois"]],
                          [hb.to_device(k) for k in g[f"{scheme}_gks"]], out)
     assert np.array_equal(hb.to_host(out)[0], g[f"{scheme}_out"])
+
+
+# ---- hoisted linear transform (fhe_linear_hoisted[_at], CKKS): sum_r pt_r (.) rot_r(ct)
+@pytest.mark.parametrize("log_n,L,K,dnum,n_ct,steps,lvl", [
+    (16, 12, 4, 3, 2, (1, 2, -1, 5), None),
+    (16, 12, 4, 3, 1, (1, 3, -2), 7),
+    (12, 5, 2, 3, 3, tuple(range(1, 19)), None),  # two chunks of the 16-element kernel, one-pass ModDown
+])
+def test_linear_transform_hoisted(hb, log_n, L, K, dnum, n_ct, steps, lvl):
+    o = Oracle(SCHEME_CKKS, log_n, L, K, dnum)
+    c = hb.Context(SCHEME_CKKS, log_n, L, K, dnum, moduli=o.moduli)
+    m = L if lvl is None else lvl
+    ct = o.uniform((n_ct, 2, m, o.n), seed=2000 + log_n + m)
+    gs = [o.galois_elt(k) for k in steps]
+    gks = [o.uniform(o.key_shape(), seed=2010 + i) for i in range(len(gs))]
+    pts = [o.uniform((L + K, o.n), seed=2100 + i) for i in range(len(gs))]
+    want = o.linear_hoisted(ct, gs, np.stack(gks), np.stack(pts), m)
+    d_gk = [hb.to_device(k) for k in gks]
+    d_pt = [hb.to_device(p) for p in pts]
+    out = hb.empty(ct.shape)
+    if lvl is None:
+        c.linear_hoisted(hb.to_device(ct), gs, d_gk, d_pt, out)
+        io = hb.to_device(ct)
+        c.linear_hoisted(io, gs, d_gk, d_pt, io)  # in place
+        assert np.array_equal(hb.to_host(io), want)
+    else:
+        c.linear_hoisted_at(hb.to_device(ct), gs, d_gk, d_pt, out, lvl)
+    assert np.array_equal(hb.to_host(out), want)
+
+
+def test_linear_transform_hoisted_bfv_unsupported(hb):
+    import ctypes as C
+    lib = hb.load_library()
+    bfv = hb.Context(SCHEME_BFV, 12, 3, 1, 1, t=65537)
+    z = hb.empty((1, 2, 3, bfv.n))
+    k = hb.empty(bfv.key_shape())
+    p = hb.empty((4, bfv.n))
+    ga = (C.c_uint32 * 1)(5)
+    ka = (C.c_uint64 * 1)(hb._ptr(k))
+    pa = (C.c_uint64 * 1)(hb._ptr(p))
+    assert lib.fhe_linear_hoisted(bfv.h, hb._ptr(z), 1, C.addressof(ga), C.addressof(ka), C.addressof(pa),
+                                  hb._ptr(hb.empty((1, 2, 3, bfv.n))), 1) == hb.FHE_ERR_UNSUPPORTED
