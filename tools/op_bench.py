@@ -5,6 +5,7 @@
 
 *_hrot: --rot (default 4) hoisted rotations of the batch (fhe_rotate_hoisted); the rate counts rotations.
 *_rsum: the sum of --rot rotations with one ModDown (fhe_rotate_sum_hoisted); the rate counts rotations.
+ckks_lin: the hoisted linear transform of --rot plaintext-weighted rotations (fhe_linear_hoisted).
 
 --openfhe-primes: the CKKS ops on OpenFHE-style primes (q = 1 mod 2N, generic
 Montgomery path) instead of the default q = 1 (mod 2^32) family.
@@ -20,7 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("op", choices=["bfv_mul", "ckks_mul", "ckks_rot", "ckks_hrot", "bfv_rot", "bfv_hrot",
-                                       "ckks_rsum", "bfv_rsum"])
+                                       "ckks_rsum", "bfv_rsum", "ckks_lin"])
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--openfhe-primes", action="store_true")
@@ -47,13 +48,16 @@ def main():
     g = c.galois_elt(1)
     gs = [c.galois_elt(s_) for s_ in range(1, args.rot + 1)]
     outs = [hb.empty(shape) for _ in gs] if args.op.endswith("hrot") else []
-    per = len(gs) if args.op.endswith("hrot") or args.op.endswith("rsum") else 1
+    per = len(gs) if args.op.endswith(("hrot", "rsum", "lin")) else 1
+    pts = [c.fill_uniform(hb.empty((c.L + c.K, c.n)), seed=10 + i) for i in range(len(gs))] \
+        if args.op == "ckks_lin" else []
     fn = {"bfv_mul": lambda: c.mul_relin(a, b, k, out), "ckks_mul": lambda: c.mul_relin(a, b, k, out),
           "ckks_rot": lambda: c.rotate(a, g, k, out), "bfv_rot": lambda: c.rotate(a, g, k, out),
           "ckks_hrot": lambda: c.rotate_hoisted(a, gs, [k] * len(gs), outs),
           "bfv_hrot": lambda: c.rotate_hoisted(a, gs, [k] * len(gs), outs),
           "ckks_rsum": lambda: c.rotate_sum_hoisted(a, gs, [k] * len(gs), out),
-          "bfv_rsum": lambda: c.rotate_sum_hoisted(a, gs, [k] * len(gs), out)}[args.op]
+          "bfv_rsum": lambda: c.rotate_sum_hoisted(a, gs, [k] * len(gs), out),
+          "ckks_lin": lambda: c.linear_hoisted(a, gs, [k] * len(gs), pts, out)}[args.op]
     fn()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
