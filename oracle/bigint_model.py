@@ -222,7 +222,8 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = Non
     only the key rows of Q_lvl u P are used.  Returns (ks0, ks1), each lvl limbs.
     multi = [(ksk_r, g_r), ...] (double-hoisted rotation sum): the inner products
     of every key with sigma_{g_r}(ext) are summed before the one ModDown."""
-    keys = multi if multi is not None else [(ksk, ext_g)]
+    keys = [(kk[0], kk[1], kk[2] if len(kk) > 2 else None) for kk in multi] if multi is not None \
+        else [(ksk, ext_g, None)]
     L, K = (p.L if lvl is None else lvl), p.K
     mi = list(range(L)) + [p.L + k for k in range(K)]  # level space -> modulus / key row
     QP = list(range(L + K))
@@ -243,8 +244,9 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = Non
             ext[i] = dn[i]
         for i, c in zip(others, conv_n):
             ext[i] = c
-        for kr, g in keys:
-            # hoisted rotation: sigma_g applied to the digit's extension
+        for kr, g, pt in keys:
+            # hoisted rotation: sigma_g applied to the digit's extension; pt: a
+            # plaintext weight (hoisted linear transform), rows like the key's
             ex = {i: automorph_ntt(e, g) for i, e in ext.items()} if g else ext
             for b in range(2):
                 for i in QP:
@@ -252,8 +254,12 @@ def keyswitch(p: Params, d: List[List[int]], ksk, ntt_form: bool, lvl: int = Non
                     kb = kr[j][b][mi[i]]
                     e = ex[i]
                     row = acc[b][i]
+                    w = pt[mi[i]] if pt is not None else None
                     for k in range(p.n):
-                        row[k] = (row[k] + e[k] * kb[k]) % q
+                        v = e[k] * kb[k]
+                        if w is not None:
+                            v = v % q * w[k]
+                        row[k] = (row[k] + v) % q
     Pprod = math.prod(p.P)
     Qs = p.moduli[:L]
     out = []
@@ -288,6 +294,18 @@ def rotate_sum_hoisted(p: Params, ct, gs, gks):
         else:
             r0 = [automorph_coef(x, g, p.moduli[i]) for i, x in enumerate(ct[0])]
         c0 = [[(x + y) % p.moduli[i] for x, y in zip(c0[i], r0[i])] for i in range(p.L)]
+    return [c0, ks1]
+
+
+def linear_hoisted(p: Params, ct, gs, gks, pts):
+    """Hoisted linear transform (CKKS): sum_r pts[r] (.) rot_{g_r}(ct) with the
+    plaintext-weighted inner products summed before ONE ModDown.  pts[r]: L+K
+    limbs in the NTT domain."""
+    ks0, ks1 = keyswitch(p, ct[1], None, True, None, 0, list(zip(gks, gs, pts)))
+    c0 = ks0
+    for g, pt in zip(gs, pts):
+        r0 = [automorph_ntt(x, g) for x in ct[0]]
+        c0 = [[(x + y * w) % p.moduli[i] for x, y, w in zip(c0[i], r0[i], pt[i])] for i in range(p.L)]
     return [c0, ks1]
 
 

@@ -131,8 +131,10 @@ def gen_rotation_sums(rng):
     ct = [rand_limbs(rng, Q, n) for _ in range(2)]
     gs = [M.galois_elt(log_n, 1), M.galois_elt(log_n, 3), 2 * n - 1]
     gks = [[[rand_limbs(rng, Q + P, n) for _ in range(2)] for _ in range(2)] for _ in gs]
+    pts = [rand_limbs(rng, Q + P, n) for _ in gs]
     out["ckks"] = dict(moduli=arr(Q + P), ct=arr(ct), galois=np.array(gs, dtype=np.uint32), gks=arr(gks),
-                       out=arr(M.rotate_sum_hoisted(p, ct, gs, gks)))
+                       out=arr(M.rotate_sum_hoisted(p, ct, gs, gks)), pts=arr(pts),
+                       lin=arr(M.linear_hoisted(p, ct, gs, gks, pts)))
     Qb = M.gen_primes(60, log_n, 4)
     Pb = M.gen_primes(61, log_n, 2, exclude=Qb)
     Bsk = M.gen_primes(61, log_n, 5, exclude=Qb + Pb)

@@ -235,6 +235,10 @@ def test_rotation_sum_golden(hb, scheme):
     c.rotate_sum_hoisted(hb.to_device(g[f"{scheme}_ct"][None]), [int(x) for x in g[f"{scheme}_galois"]],
                          [hb.to_device(k) for k in g[f"{scheme}_gks"]], out)
     assert np.array_equal(hb.to_host(out)[0], g[f"{scheme}_out"])
+    if scheme == "ckks":
+        c.linear_hoisted(hb.to_device(g["ckks_ct"][None]), [int(x) for x in g["ckks_galois"]],
+                         [hb.to_device(k) for k in g["ckks_gks"]], [hb.to_device(p) for p in g["ckks_pts"]], out)
+        assert np.array_equal(hb.to_host(out)[0], g["ckks_lin"])
 
 
 # ---- hoisted linear transform (fhe_linear_hoisted[_at], CKKS): sum_r pt_r (.) rot_r(ct)

@@ -157,3 +157,6 @@ def test_rotation_sum_golden(scheme):
         o = Oracle(SCHEME_BFV, int(g["log_n"]), 4, 2, 2, t=65537, moduli=mods)
     out = o.rotate_sum_hoisted(g[f"{scheme}_ct"][None], g[f"{scheme}_galois"], g[f"{scheme}_gks"])
     assert np.array_equal(out[0], g[f"{scheme}_out"])
+    if scheme == "ckks":  # the hoisted linear transform on the same inputs, plaintext-weighted
+        lin = o.linear_hoisted(g["ckks_ct"][None], g["ckks_galois"], g["ckks_gks"], g["ckks_pts"])
+        assert np.array_equal(lin[0], g["ckks_lin"])
