@@ -157,7 +157,7 @@ def main():
     import torch.distributed as dist
 
     import herdsman_amd.backend as hb
-    from herdsman_amd.dist import broadcast_key, max_over_ranks
+    from herdsman_amd.dist import broadcast_key, max_over_ranks, shard_range
     from herdsman_amd.dist import world as dist_world
 
     rank, local, world = dist_world()
@@ -263,23 +263,28 @@ def main():
     else:
         per_rank = [(my * steps / mine) if mine > 0 else 0.0]
     value = G * steps / elapsed if steps else 0.0
-
-    # ---- per-rank output check: every lane context of every rank recomputes the
-    # committed metric digest case with the broadcast key (after the timed region)
-    mine_ok = rank_self_check(hb, lanes, rlk, dev)
-    per_rank_ok = [mine_ok]
+    # every rank's shard (first row, size) and the ct-mults its step actually
+    # issued: the line shows each rank's share, and a plan that does not cover
+    # the global batch exactly once fails the run (exit 5)
+    shard = {"first": shard_range(G, world, rank)[0], "size": my, "issued": sum(hi - lo for _, lo, hi in plan)}
+    shards = [shard]
     if world > 1:
-        per_rank_ok = [None] * world
-        dist.all_gather_object(per_rank_ok, mine_ok)
+        shards = [None] * world
+        dist.all_gather_object(shards, shard)
+    shards_ok = (sum(s_["issued"] for s_ in shards) == G and all(s_["issued"] == s_["size"] for s_ in shards)
+                 and all(shards[r]["first"] + shards[r]["size"] == (shards[r + 1]["first"] if r + 1 < world else G)
+                         for r in range(world)))
 
-    # ---- dominant kernel group: forward NTT over the ModUp-sized wave (36 limbs per ct)
+    # ---- dominant kernel group: forward NTT over the ModUp-sized wave (36 limbs per ct),
+    # right after the timed steps: the timed launches follow the warm-up ones with no
+    # idle gap at 1 rank (an idle GPU re-ramps its clock: +1.5% on the launch time)
     limbs = B * 3 * L
     x = hb.empty((B * 3, L, n), device=dev)
     ctx.fill_uniform(x, seed=99)
     for _ in range(3):
         ctx.ntt_fwd(x)
-    torch.cuda.synchronize(dev)
     if world > 1:
+        torch.cuda.synchronize(dev)
         dist.barrier()  # every rank's NTT loop runs at the same time (the N-GPU NTT/s)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)  # the stream the NTT kernels are launched on (ctx.set_stream above)
@@ -294,6 +299,14 @@ def main():
     if world > 1:
         ntt_rates = [None] * world
         dist.all_gather_object(ntt_rates, limbs / (ntt_ms * 1e-3))
+    # ---- per-rank output check: every lane context of every rank recomputes the
+    # committed metric digest case with the broadcast key (after the timed regions)
+    mine_ok = rank_self_check(hb, lanes, rlk, dev)
+    per_rank_ok = [mine_ok]
+    if world > 1:
+        per_rank_ok = [None] * world
+        dist.all_gather_object(per_rank_ok, mine_ok)
+
     algo_per_limb = 2 * n * 8
     algo_bytes = limbs * algo_per_limb
     achieved = algo_bytes / (ntt_ms * 1e-3) / 1e9
@@ -339,7 +352,10 @@ def main():
                 "workload": f"C5: {G} independent CKKS ct-mult+relin per step, sharded over {world} rank(s)",
                 "log_n": LOG_N, "L": L, "K": K, "dnum": DNUM,
                 "q_bits": 60, "p_bits": 61,
-                "global_batch": G, "batch_per_gpu": my, "wave": B, "waves_per_step": waves,
+                "global_batch": G, "batch_per_gpu": my, "batch_per_rank": [s_["size"] for s_ in shards],
+                "shard_first_per_rank": [s_["first"] for s_ in shards],
+                "issued_per_step_per_rank": [s_["issued"] for s_ in shards], "shards_cover_batch": shards_ok,
+                "wave": B, "waves_per_step": waves,
                 "resident_pool": P, "streams_per_gpu": S,
                 "parallelism": f"shard{world}", "ranks": world,
             },
@@ -364,6 +380,11 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not shards_ok:
+        if rank == 0:
+            print(f"bench.py: the ranks' shards do not cover the global batch {G} exactly once: {shards}",
+                  file=sys.stderr, flush=True)
+        return 5
     if not all(v["ok"] for v in per_rank_ok):
         if rank == 0:
             print(f"bench.py: output digest mismatch on rank(s) "

@@ -62,6 +62,7 @@ SIGNATURES = {
     "fhe_host_free": (C.c_int, [_vp, _vp]),
     "fhe_memcpy_h2d_async": (C.c_int, [_vp, _vp, _vp, _sz]),
     "fhe_memcpy_d2h_async": (C.c_int, [_vp, _vp, _vp, _sz]),
+    "fhe_memcpy_d2d_async": (C.c_int, [_vp, _vp, _vp, _sz]),
     "fhe_use_own_stream": (C.c_int, [_vp]),
     "fhe_mark": (C.c_int, [_vp, C.c_uint32]),
     "fhe_wait_mark": (C.c_int, [_vp, C.c_uint32]),

@@ -549,6 +549,11 @@ int fhe_memcpy_d2h_async(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
   DeviceBind bind(c);
   return fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream), "d2h async");
 }
+int fhe_memcpy_d2d_async(fhe_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return FHE_ERR_INVALID;
+  DeviceBind bind(c);
+  return fhe_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream), "d2d async");
+}
 int fhe_use_own_stream(fhe_ctx *c) {
   if (!c) return FHE_ERR_INVALID;
   DeviceBind bind(c);
@@ -754,6 +759,11 @@ static int rot_sum(fhe_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_
     if (!gks[r]) return fhe_fail(c, FHE_ERR_INVALID, "null key");
   }
   const size_t cw = (size_t)2 * c->L * c->n;
+  // in place (out == ct) or apart: the work runs in chunks of kCtChunk
+  // ciphertexts, and a partly overlapping out would overwrite rows of ct that
+  // a later chunk still reads
+  if (out != ct && !(out + n_ct * cw <= ct || ct + n_ct * cw <= out))
+    return fhe_fail(c, FHE_ERR_INVALID, "rotation sum output partly overlaps its input (use out == ct or apart)");
   for (uint32_t c0 = 0; c0 < n_ct; c0 += kCtChunk) {
     const uint32_t m = std::min(kCtChunk, n_ct - c0);
     int rc = rotate_sum_hoisted_impl(c, ct + c0 * cw, n_rot, galois, gks, out + c0 * cw, m, pts);
@@ -772,14 +782,21 @@ static int from_view(fhe_ctx *c, fhe_ctx *v, int rc) {
   return rc;
 }
 
+// BFV ciphertexts live at level L only (ctx_level): the element-wise ops say so too
+static int ew_level_ok(fhe_ctx *c, uint32_t level) {
+  if (level == 0 || level > c->L) return fhe_fail(c, FHE_ERR_INVALID, "level must be in [1, L]");
+  if (c->params.scheme == FHE_SCHEME_BFV && level != c->L)
+    return fhe_fail(c, FHE_ERR_UNSUPPORTED, "BFV ciphertexts have no reduced levels (level must be L)");
+  return FHE_OK;
+}
 int fhe_add_at(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct, uint32_t level) {
   if (!c) return FHE_ERR_INVALID;
-  if (level == 0 || level > c->L) return fhe_fail(c, FHE_ERR_INVALID, "level must be in [1, L]");
+  if (int rc = ew_level_ok(c, level)) return rc;
   return ew(c, EwOp::Add, a, b, out, 2 * n_ct, 0, level);
 }
 int fhe_sub_at(fhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, uint32_t n_ct, uint32_t level) {
   if (!c) return FHE_ERR_INVALID;
-  if (level == 0 || level > c->L) return fhe_fail(c, FHE_ERR_INVALID, "level must be in [1, L]");
+  if (int rc = ew_level_ok(c, level)) return rc;
   return ew(c, EwOp::Sub, a, b, out, 2 * n_ct, 0, level);
 }
 int fhe_mul_relin_at(fhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk, uint64_t *out,

@@ -230,6 +230,18 @@ __device__ __forceinline__ u64 ld_d(const u64 *base, u32 off) {
   return __builtin_nontemporal_load((const u64 *)((const char *)base + off));
 }
 __device__ __forceinline__ void st_b(u64 *base, u32 off, u64 v) { *(u64 *)((char *)base + off) = v; }
+#ifndef NTT_NTST
+#define NTT_NTST 3  // bit 0: the passes' own data stores non-temporal; bit 1: the fused epilogue/prologue outputs too
+#endif
+// a pass's own data words (bit 0) and its fused outputs (bit 1) are written once
+__device__ __forceinline__ void st_d(u64 *base, u32 off, u64 v) {
+  if constexpr (NTT_NTST & 1) __builtin_nontemporal_store(v, (u64 *)((char *)base + off));
+  else st_b(base, off, v);
+}
+__device__ __forceinline__ void st_e(u64 *base, u32 off, u64 v) {
+  if constexpr (NTT_NTST & 2) __builtin_nontemporal_store(v, (u64 *)((char *)base + off));
+  else st_b(base, off, v);
+}
 
 #ifndef LDS_PAD
 #define LDS_PAD 1  // 0: unpadded exchange tile (32 KiB at S = 8, W = 16: 5 workgroups per CU, bank conflicts)
@@ -566,9 +578,9 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
           }
           u64 ks = harvey_csub(mont_mul<SP>((acc + cb1) + ~v, ep.pinv, mi), nq1);
           if (ep.add) ks = add_mod(ks, pb[r], q);
-          st_b(ep.out + kr, voff, ks);
+          st_e(ep.out + kr, voff, ks);
         } else {
-          st_b(data + kr, voff, v);
+          st_d(data + kr, voff, v);
         }
       }
     } else {
@@ -577,7 +589,7 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
       // thread sits at voff + k_reg(r) << LS -- a compile-time offset on the
       // scalar base, so the address costs no VALU
 #pragma unroll
-      for (int r = 0; r < R; ++r) st_b(data + ((size_t)GP::k_reg(r) << PG::LS), voff, x[r]);
+      for (int r = 0; r < R; ++r) st_d(data + ((size_t)GP::k_reg(r) << PG::LS), voff, x[r]);
     }
   }
 }
@@ -623,13 +635,13 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         }
         const u64 a0 = op[r % (PD + 1)][0], a1 = op[r % (PD + 1)][1];
         const u64 b0 = op[r % (PD + 1)][2], b1 = op[r % (PD + 1)][3];
-        st_b(ep.o0 + kr, voff, mul_mod<SP>(a0, b0, mi));
+        st_e(ep.o0 + kr, voff, mul_mod<SP>(a0, b0, mi));
         U128 s = mul128(a0, b1);
         mac128(s, a1, b0);
-        st_b(ep.o1 + kr, voff, reduce128<SP>(s, mi));
+        st_e(ep.o1 + kr, voff, reduce128<SP>(s, mi));
         const u64 t = mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi);  // d2 in [0, 2q)
         x[r] = csub(t, mi.q);
-        st_b(ep.ext + kr, voff, csub(mont_mul<SP>(t, mi.r2, mi), mi.q));  // d2 R
+        st_e(ep.ext + kr, voff, csub(mont_mul<SP>(t, mi.r2, mi), mi.q));  // d2 R
       }
     } else if constexpr (EPI == PRO_BFVT) {
       // the BFV tensor formulas at the coalesced positions; e is per workgroup
@@ -669,9 +681,9 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
           y[(r + PD) % (PD + 1)][0] = ep.o0 ? ld_b(ep.a0, sn) : 0, y[(r + PD) % (PD + 1)][1] = ld_b(ep.a1, sn);
         }
         const u64 y0 = y[r % (PD + 1)][0], y1 = y[r % (PD + 1)][1];
-        if (ep.o0) st_b(ep.o0 + kr, voff, y0);
+        if (ep.o0) st_e(ep.o0 + kr, voff, y0);
         x[r] = y1;
-        st_b(ep.ext + kr, voff, csub63(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
+        st_e(ep.ext + kr, voff, csub63(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
       }
     } else if constexpr (is_ksp(EPI)) {
       // acc_P = sum_j ext_j ksk_j R^-1 (ks_inner_kernel; ext carries R) at the

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <list>
 #include <exception>
 #include <stdexcept>
 #include <string>
@@ -301,8 +302,16 @@ class IoPool {
   std::exception_ptr err_;
 };
 
-// f(i) for i in [0, n) on up to `threads` threads: the calling (lane) thread's
-// persistent IoPool of that size
+// the calling thread's persistent IoPool of `threads` threads: one per lane (or
+// flusher) thread, shared by every kind of job it runs (a thread_local inside
+// the parallel_for template would be one pool per lambda type)
+IoPool &thread_pool(unsigned threads) {
+  thread_local std::unique_ptr<IoPool> pool;
+  if (!pool || pool->size() != threads) pool = std::make_unique<IoPool>(threads);
+  return *pool;
+}
+
+// f(i) for i in [0, n) on up to `threads` threads of the calling thread's pool
 template <class F>
 void parallel_for(size_t n, unsigned threads, F f) {
   threads = std::max(1u, threads);
@@ -310,9 +319,7 @@ void parallel_for(size_t n, unsigned threads, F f) {
     for (size_t i = 0; i < n; ++i) f(i);
     return;
   }
-  thread_local std::unique_ptr<IoPool> pool;
-  if (!pool || pool->size() != threads) pool = std::make_unique<IoPool>(threads);
-  pool->run(n, std::function<void(size_t)>(f));
+  thread_pool(threads).run(n, std::function<void(size_t)>(f));
 }
 
 void ck(fhe_ctx *c, int rc, const char *what) {
@@ -457,6 +464,36 @@ double secs_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+struct FrameBudget;
+
+// A MapTask's output partition kept in HBM (GpuWorkerGroupConfig::
+// resident_frame_bytes): `rows` ciphertexts at one level, row r at p + r cw.
+struct ResidentFrame {
+  std::string key;  // session / frame / partition
+  int device = 0, schema = 0;
+  uint32_t level = 0;
+  size_t rows = 0, cw = 0;
+  fhe_ctx *ctx = nullptr;  // the allocating lane's context (freed through it)
+  uint64_t *p = nullptr;
+  size_t bytes() const { return rows * cw * 8; }
+  // write-behind: where and how the flusher writes the partition file
+  std::filesystem::path file;
+  CtHeader header{};
+  bool durable = false;
+  // the device budget this frame's bytes are charged to (cleared when it is
+  // evicted; the memory itself goes when the last reader drops the frame)
+  FrameBudget *budget = nullptr;
+  ~ResidentFrame();
+};
+
+// per device: resident frames by key, least recently used last, and the bytes
+// charged (frames in the map plus outputs still being produced)
+struct FrameBudget {
+  std::map<std::string, std::shared_ptr<ResidentFrame>> map;
+  std::list<std::string> lru;
+  uint64_t bytes = 0;
+};
+
 }  // namespace
 
 struct GpuWorkerGroup::Job {
@@ -481,7 +518,98 @@ struct GpuWorkerGroup::Device {
   std::map<std::pair<std::string, int>, std::shared_ptr<KeySet>> keys;
 };
 
-GpuWorkerGroup::GpuWorkerGroup(GpuWorkerGroupConfig config) : config_(std::move(config)) {
+// Resident frames of every device and the write-behind flusher's queue.  One
+// mutex: lookups happen once per task, not per row.
+struct GpuWorkerGroup::Frames {
+  std::mutex m;
+  std::condition_variable cv;  // flush queue changes, files committed
+  std::map<int, FrameBudget> dev;
+  std::deque<std::shared_ptr<ResidentFrame>> queue;              // waiting for the flusher
+  std::map<std::string, std::shared_ptr<ResidentFrame>> pending;  // queued or being written
+  bool stop = false, failed = false;
+  std::map<std::pair<int, int>, fhe_ctx *> flush_ctx;  // (device, schema) -> the flusher's context
+  StageStats st;                                      // flushed rows and time
+
+  // charge `need` bytes to the device, evicting least recently used frames
+  // (their memory is freed once no task reads them); false if it cannot fit
+  FrameBudget *reserve(int device, uint64_t need, uint64_t cap, std::vector<std::shared_ptr<ResidentFrame>> &evicted) {
+    std::lock_guard lk(m);
+    FrameBudget &b = dev[device];
+    if (need > cap) return nullptr;
+    while (b.bytes + need > cap && !b.lru.empty()) {
+      auto it = b.map.find(b.lru.back());
+      b.lru.pop_back();
+      if (it == b.map.end()) continue;
+      b.bytes -= it->second->bytes();
+      it->second->budget = nullptr;
+      evicted.push_back(std::move(it->second));
+      b.map.erase(it);
+    }
+    if (b.bytes + need > cap) return nullptr;
+    b.bytes += need;
+    return &b;
+  }
+  void publish(const std::shared_ptr<ResidentFrame> &f, std::vector<std::shared_ptr<ResidentFrame>> &dropped) {
+    std::lock_guard lk(m);
+    FrameBudget &b = dev[f->device];
+    auto it = b.map.find(f->key);
+    if (it != b.map.end()) {
+      b.bytes -= it->second->bytes();
+      it->second->budget = nullptr;
+      dropped.push_back(std::move(it->second));
+      b.lru.remove(f->key);
+    }
+    b.map[f->key] = f;
+    b.lru.push_front(f->key);
+  }
+  // the partition is being rewritten: no device may serve its old contents
+  void drop(const std::string &key, std::vector<std::shared_ptr<ResidentFrame>> &dropped) {
+    std::lock_guard lk(m);
+    for (auto &kv : dev) {
+      FrameBudget &b = kv.second;
+      auto it = b.map.find(key);
+      if (it == b.map.end()) continue;
+      b.bytes -= it->second->bytes();
+      it->second->budget = nullptr;
+      dropped.push_back(std::move(it->second));
+      b.map.erase(it);
+      b.lru.remove(key);
+    }
+  }
+  std::shared_ptr<ResidentFrame> lookup(int device, const std::string &key, int schema) {
+    std::lock_guard lk(m);
+    FrameBudget &b = dev[device];
+    auto it = b.map.find(key);
+    if (it == b.map.end() || it->second->schema != schema) return nullptr;
+    b.lru.remove(key);
+    b.lru.push_front(key);
+    return it->second;
+  }
+  // a file still being written behind is read only once it is committed
+  void wait_file(const std::string &key) {
+    std::unique_lock lk(m);
+    cv.wait(lk, [&] { return !pending.count(key); });
+  }
+};
+
+ResidentFrame::~ResidentFrame() {
+  if (p) fhe_dev_free(ctx, p);
+}
+
+namespace {
+// release the bytes of a frame that never reached the map (a failed task)
+void unreserve(std::mutex &m, FrameBudget &b, ResidentFrame &f) {
+  std::lock_guard lk(m);
+  if (f.budget) b.bytes -= f.bytes();
+  f.budget = nullptr;
+}
+
+std::string frame_key(const herd::common::UUID &session, const herd::common::DataFramePtr &p) {
+  return session.as_string() + "/" + p.uuid.as_string() + "/" + std::to_string(p.partition);
+}
+}  // namespace
+
+GpuWorkerGroup::GpuWorkerGroup(GpuWorkerGroupConfig config) : config_(std::move(config)), frames_(new Frames) {
   if (config_.devices.empty()) throw std::invalid_argument("GpuWorkerGroup needs at least one device");
   if (!circuits_lowerable())
     std::fprintf(stderr,
@@ -498,6 +626,7 @@ GpuWorkerGroup::GpuWorkerGroup(GpuWorkerGroupConfig config) : config_(std::move(
   for (auto &d : devices_)
     for (auto &l : d->lanes) l->thread = std::thread([this, dp = d.get(), lp = l.get()] { lane_loop(*dp, *lp); });
   completion_thread_ = std::thread([this] { completion_loop(); });
+  if (config_.write_behind) flush_thread_ = std::thread([this] { flush_loop(); });
 }
 
 GpuWorkerGroup::~GpuWorkerGroup() {
@@ -510,8 +639,29 @@ GpuWorkerGroup::~GpuWorkerGroup() {
   }
   for (auto &d : devices_)
     for (auto &l : d->lanes) l->thread.join();
-  // teardown order: keys and lane buffers are freed through their contexts,
-  // so they go before the contexts
+  // files written behind are committed before the group goes
+  if (flush_thread_.joinable()) {
+    flush_frames();
+    {
+      std::lock_guard lk(frames_->m);
+      frames_->stop = true;
+    }
+    frames_->cv.notify_all();
+    flush_thread_.join();
+  }
+  // teardown order: resident frames, keys and lane buffers are freed through
+  // their contexts, so they go before the contexts
+  {
+    std::map<int, FrameBudget> gone;
+    {
+      std::lock_guard lk(frames_->m);
+      gone.swap(frames_->dev);
+      for (auto &kv : gone)
+        for (auto &f : kv.second.map) f.second->budget = nullptr;
+    }
+  }
+  for (auto &kv : frames_->flush_ctx) fhe_ctx_destroy(kv.second);
+  frames_->flush_ctx.clear();
   for (auto &d : devices_) {
     d->keys.clear();
     for (auto &l : d->lanes) {
@@ -537,13 +687,32 @@ GpuWorkerGroup::~GpuWorkerGroup() {
 }
 
 StageStats GpuWorkerGroup::stage_stats() {
-  std::lock_guard lk(stats_m_);
-  return stats_;
+  StageStats st;
+  {
+    std::lock_guard lk(stats_m_);
+    st = stats_;
+  }
+  std::lock_guard lk(frames_->m);
+  st.flushed_rows += frames_->st.flushed_rows;
+  st.flush_s += frames_->st.flush_s;
+  return st;
 }
 
 void GpuWorkerGroup::reset_stage_stats() {
-  std::lock_guard lk(stats_m_);
-  stats_ = StageStats{};
+  {
+    std::lock_guard lk(stats_m_);
+    stats_ = StageStats{};
+  }
+  std::lock_guard lk(frames_->m);
+  frames_->st = StageStats{};
+}
+
+bool GpuWorkerGroup::flush_frames() {
+  std::unique_lock lk(frames_->m);
+  frames_->cv.wait(lk, [&] { return frames_->queue.empty() && frames_->pending.empty(); });
+  const bool ok = !frames_->failed;
+  frames_->failed = false;
+  return ok;
 }
 
 std::size_t GpuWorkerGroup::concurrent_workers() const noexcept {
@@ -747,10 +916,13 @@ const DevBuf &galois_key(const SchemaCtx &s, const KeySet &ks, int32_t steps, ui
 // the partition file into slot k % 2's pinned buffers (pread), then enqueue
 // H2D, the program's ops and D2H on the lane's stream and mark the slot.
 // Nothing waits for the GPU here.
-// One operand of the stack program: a batch of n ciphertexts at one level.
+// One operand of the stack program: a batch of n ciphertexts at one level,
+// in an arena buffer or (view) in a resident frame, which no op writes to.
 struct StackCt {
   ArenaBuf buf;
   uint32_t level = 0;
+  const uint64_t *view = nullptr;
+  const uint64_t *ptr() const { return view ? view : buf.p; }
 };
 
 // The level-m copy of a (the first m limbs of each poly), or a itself
@@ -758,8 +930,77 @@ StackCt at_level(LaneSchema &ls, StackCt a, uint32_t m, size_t n) {
   if (a.level == m) return a;
   const SchemaCtx &s = ls.s;
   StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
-  ck(s.ctx, fhe_level_reduce(s.ctx, a.buf.p, o.buf.p, (uint32_t)n, a.level, m), "level_reduce");
+  ck(s.ctx, fhe_level_reduce(s.ctx, a.ptr(), o.buf.p, (uint32_t)n, a.level, m), "level_reduce");
   return o;
+}
+
+// Where a MapTask's rows come from and where its results go.
+struct MapIo {
+  const PartitionIndex *rows = nullptr;  // the input partition file, or
+  std::shared_ptr<ResidentFrame> in;     // the input partition resident in HBM (one ciphertext per row)
+  std::shared_ptr<ResidentFrame> out;    // this task's output kept resident (null: not kept)
+  bool write_file = true;                // the lane copies results back and writes the file
+  size_t row_count() const { return in ? in->rows : rows->size(); }
+};
+
+// byte offset and level of every input index the program pushes, from row r0
+// (a resident row is one ciphertext at the frame's level)
+void input_layout(const SchemaCtx &s, const MapIo &io, int32_t max_in, size_t r0, std::vector<size_t> &off,
+                  std::vector<uint32_t> &level) {
+  off.clear();
+  level.clear();
+  if (io.in) {
+    if (max_in > 0) throw std::runtime_error("row holds fewer ciphertexts than the circuit reads");
+    off.push_back(0);
+    level.push_back(io.in->level);
+    return;
+  }
+  for (size_t o = 0; (int32_t)off.size() <= max_in;) {
+    CtHeader h;
+    io.rows->read(r0, o, &h, sizeof(h));
+    const uint32_t m = check_ct_header(s, h);
+    off.push_back(o);
+    level.push_back(m);
+    o += sizeof(h) + s.ct_words(m) * 8;
+  }
+}
+
+int32_t max_input(const std::vector<Instr> &prog) {
+  int32_t max_in = -1;
+  for (const auto &ins : prog)
+    if (ins.op == Op::PUSH_INPUT) max_in = std::max(max_in, ins.arg);
+  return max_in;
+}
+
+// the level of the program's result for inputs at these levels (the ops'
+// level rules below), or 0 if the program is malformed (the batch then fails
+// where it runs)
+uint32_t program_level(const std::vector<Instr> &prog, const std::vector<uint32_t> &in_level) {
+  std::vector<uint32_t> st;
+  for (const auto &ins : prog) {
+    switch (ins.op) {
+      case Op::PUSH_INPUT:
+        if (ins.arg < 0 || (size_t)ins.arg >= in_level.size()) return 0;
+        st.push_back(in_level[ins.arg]);
+        break;
+      case Op::ADD:
+      case Op::SUB:
+      case Op::MUL_RELIN: {
+        if (st.size() < 2) return 0;
+        const uint32_t b = st.back();
+        st.pop_back();
+        st.back() = std::min(st.back(), b);
+        break;
+      }
+      case Op::RESCALE:
+        if (st.empty() || st.back() < 2) return 0;
+        st.back() -= 1;
+        break;
+      default:
+        if (st.empty()) return 0;
+    }
+  }
+  return st.size() == 1 ? st.back() : 0;
 }
 
 // Batch k of a MapTask, first half: read the rows' ciphertexts straight from
@@ -768,43 +1009,47 @@ StackCt at_level(LaneSchema &ls, StackCt a, uint32_t m, size_t n) {
 // Nothing waits for the GPU here.  A row holds its ciphertexts back to back,
 // each CtHeader + 2 m N words at its own level m (CKKS); the batch's first
 // row fixes each input's level, and every row must match it.
-void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vector<Instr> &prog,
-                       const PartitionIndex &rows, size_t r0, size_t n, unsigned io_threads, StageStats &st) {
+void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vector<Instr> &prog, const MapIo &io,
+                       size_t r0, size_t n, unsigned io_threads, StageStats &st) {
   const SchemaCtx &s = ls.s;
   Slot &sl = ls.slot[si];
   sl.r0 = r0;
   sl.n = n;
-  // byte offset and level of every input index the program pushes
-  int32_t max_in = -1;
-  for (const auto &ins : prog)
-    if (ins.op == Op::PUSH_INPUT) max_in = std::max(max_in, ins.arg);
   std::vector<size_t> in_off;
   std::vector<uint32_t> in_level;
-  for (size_t off = 0; (int32_t)in_off.size() <= max_in;) {
-    CtHeader h;
-    rows.read(r0, off, &h, sizeof(h));
-    const uint32_t m = check_ct_header(s, h);
-    in_off.push_back(off);
-    in_level.push_back(m);
-    off += sizeof(h) + s.ct_words(m) * 8;
-  }
+  input_layout(s, io, max_input(prog), r0, in_off, in_level);
   std::vector<StackCt> stack;
   size_t push = 0;
   double read_s = 0;
   const auto t_enq = std::chrono::steady_clock::now();
+  if (io.in) st.resident_rows += n;
   for (const auto &ins : prog) {
     switch (ins.op) {
       case Op::PUSH_INPUT: {
         if (ins.arg < 0) throw std::runtime_error("negative input index");
         const uint32_t m = in_level[ins.arg];
         const size_t cw = s.ct_words(m), off = in_off[ins.arg];
+        if (io.in) {  // resident: the rows are already in HBM, in batch order
+          StackCt d;
+          d.level = m;
+          d.view = io.in->p + r0 * io.in->cw;
+          stack.push_back(std::move(d));
+          break;
+        }
         if (sl.in.size() <= push) sl.in.push_back(std::make_unique<Pinned>());
         uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[push++]->reserve(s.ctx, cw * n * 8));
         const auto t_r = std::chrono::steady_clock::now();
+        const PartitionIndex &rows = *io.rows;
+        // every row's header is checked on the way (the first row fixed the
+        // offsets: a row whose earlier ciphertexts sit at other levels fails
+        // here, at the first input whose header does not match)
         parallel_for(n, io_threads, [&](size_t r) {
           CtHeader h;
           rows.read(r0 + r, off, &h, sizeof(h));
-          if (check_ct_header(s, h) != m) throw std::runtime_error("rows of a batch differ in ciphertext level");
+          if (h.magic != kCtMagic || h.n_limbs != m)
+            throw std::runtime_error("rows of a batch differ in ciphertext level (input " + std::to_string(ins.arg) +
+                                     " of row " + std::to_string(r0 + r) + ")");
+          check_ct_header(s, h);
           rows.read(r0 + r, off + sizeof(h), host + r * cw, cw * 8);
         });
         read_s += secs_since(t_r);
@@ -825,11 +1070,11 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
         a = at_level(ls, std::move(a), m, n);
         b = at_level(ls, std::move(b), m, n);
         StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
-        if (ins.op == Op::ADD) ck(s.ctx, fhe_add_at(s.ctx, a.buf.p, b.buf.p, o.buf.p, (uint32_t)n, m), "add");
-        else if (ins.op == Op::SUB) ck(s.ctx, fhe_sub_at(s.ctx, a.buf.p, b.buf.p, o.buf.p, (uint32_t)n, m), "sub");
+        if (ins.op == Op::ADD) ck(s.ctx, fhe_add_at(s.ctx, a.ptr(), b.ptr(), o.buf.p, (uint32_t)n, m), "add");
+        else if (ins.op == Op::SUB) ck(s.ctx, fhe_sub_at(s.ctx, a.ptr(), b.ptr(), o.buf.p, (uint32_t)n, m), "sub");
         else {
           if (!ks.relin.p) throw std::runtime_error("no relinearisation key");
-          ck(s.ctx, fhe_mul_relin_at(s.ctx, a.buf.p, b.buf.p, ks.relin.p, o.buf.p, (uint32_t)n, m), "mul_relin");
+          ck(s.ctx, fhe_mul_relin_at(s.ctx, a.ptr(), b.ptr(), ks.relin.p, o.buf.p, (uint32_t)n, m), "mul_relin");
         }
         stack.push_back(std::move(o));
         break;
@@ -840,7 +1085,7 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
         const DevBuf &gk = galois_key(s, ks, ins.arg, &g);
         const uint32_t m = stack.back().level;
         StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
-        ck(s.ctx, fhe_rotate_at(s.ctx, stack.back().buf.p, g, gk.p, o.buf.p, (uint32_t)n, m), "rotate");
+        ck(s.ctx, fhe_rotate_at(s.ctx, stack.back().ptr(), g, gk.p, o.buf.p, (uint32_t)n, m), "rotate");
         stack.back() = std::move(o);
         break;
       }
@@ -861,7 +1106,7 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
           gs.push_back(g);
         }
         if (gs.empty()) break;  // mask 1: the input itself
-        const uint64_t *top = stack.back().buf.p;
+        const uint64_t *top = stack.back().ptr();
         StackCt o{ArenaBuf(*ls.arena, s.ct_words(m) * n), m};
         ck(s.ctx, fhe_rotate_sum_hoisted_at(s.ctx, top, (uint32_t)gs.size(), gs.data(), gks.data(), o.buf.p,
                                             (uint32_t)n, m), "rotate_sum_hoisted");
@@ -874,7 +1119,7 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
         const uint32_t m = stack.back().level;
         if (m < 2) throw std::runtime_error("rescale of a level-1 ciphertext");
         StackCt o{ArenaBuf(*ls.arena, s.ct_words(m - 1) * n), m - 1};
-        ck(s.ctx, fhe_rescale(s.ctx, stack.back().buf.p, o.buf.p, (uint32_t)n, m), "rescale");
+        ck(s.ctx, fhe_rescale(s.ctx, stack.back().ptr(), o.buf.p, (uint32_t)n, m), "rescale");
         stack.back() = std::move(o);
         break;
       }
@@ -885,8 +1130,14 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
   if (stack.size() != 1) throw std::runtime_error("circuit must leave exactly one ciphertext");
   sl.out_level = stack.back().level;
   const size_t cw = s.ct_words(sl.out_level);
-  uint64_t *host = reinterpret_cast<uint64_t *>(sl.out.reserve(s.ctx, cw * n * 8));
-  ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, host, stack.back().buf.p, cw * n * 8), "d2h");
+  if (io.out) {  // kept resident for the stage that reads this partition
+    if (io.out->level != sl.out_level) throw std::runtime_error("resident frame level mismatch");
+    ck(s.ctx, fhe_memcpy_d2d_async(s.ctx, io.out->p + r0 * io.out->cw, stack.back().ptr(), cw * n * 8), "d2d");
+  }
+  if (io.write_file) {
+    uint64_t *host = reinterpret_cast<uint64_t *>(sl.out.reserve(s.ctx, cw * n * 8));
+    ck(s.ctx, fhe_memcpy_d2h_async(s.ctx, host, stack.back().ptr(), cw * n * 8), "d2h");
+  }
   // the device buffers go back to the arena now: later ops that reuse them are
   // ordered after this batch's copies by the stream
   ck(s.ctx, fhe_mark(s.ctx, (uint32_t)si), "mark");
@@ -896,23 +1147,24 @@ void enqueue_map_batch(LaneSchema &ls, int si, const KeySet &ks, const std::vect
 
 // Second half: wait for the slot's mark (its D2H has landed, its H2D sources
 // are free again) and append the batch's rows to the output partition.
-void finish_map_batch(LaneSchema &ls, int si, PartitionWriter &out, unsigned io_threads, StageStats &st) {
+void finish_map_batch(LaneSchema &ls, int si, PartitionWriter *out, unsigned io_threads, StageStats &st) {
   const SchemaCtx &s = ls.s;
   Slot &sl = ls.slot[si];
   auto t0 = std::chrono::steady_clock::now();
   ck(s.ctx, fhe_wait_mark(s.ctx, (uint32_t)si), "batch wait");
   st.wait_s += secs_since(t0);
+  st.batches += 1;
+  st.rows += sl.n;
+  if (!out) return;  // write-behind: the flusher writes the file from the resident frame
   t0 = std::chrono::steady_clock::now();
   const size_t cw = s.ct_words(sl.out_level);
   const uint64_t *host = reinterpret_cast<const uint64_t *>(sl.out.p);
   const CtHeader h = ct_header(s, sl.out_level);
   const uint64_t row_bytes = 4 + sizeof(h) + cw * 8;
-  const uint64_t base = out.claim(row_bytes * sl.n);
+  const uint64_t base = out->claim(row_bytes * sl.n);
   parallel_for(sl.n, io_threads,
-               [&](size_t r) { out.write_row_at(base + r * row_bytes, {{&h, sizeof(h)}, {host + r * cw, cw * 8}}); });
+               [&](size_t r) { out->write_row_at(base + r * row_bytes, {{&h, sizeof(h)}, {host + r * cw, cw * 8}}); });
   st.write_s += secs_since(t0);
-  st.batches += 1;
-  st.rows += sl.n;
 }
 
 std::filesystem::path frame_path(const std::filesystem::path &root, const herd::common::UUID &session,
@@ -923,6 +1175,76 @@ std::filesystem::path frame_path(const std::filesystem::path &root, const herd::
 }  // namespace
 
 bool GpuWorkerGroup::circuits_lowerable() noexcept { return lowerable_v<herd::common::Circuit>; }
+
+// write-behind: the flusher copies each queued resident frame back in chunks
+// (two pinned buffers, the next chunk's D2H under the current chunk's file
+// writes) on a context and stream of its own, and commits the partition file
+void GpuWorkerGroup::flush_loop() {
+  constexpr size_t kRows = 16;
+  Pinned stage[2];
+  for (;;) {
+    std::shared_ptr<ResidentFrame> f;
+    {
+      std::unique_lock lk(frames_->m);
+      frames_->cv.wait(lk, [&] { return frames_->stop || !frames_->queue.empty(); });
+      if (frames_->queue.empty()) return;
+      f = frames_->queue.front();
+      frames_->queue.pop_front();
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    std::string err;
+    try {
+      fhe_ctx *&c = frames_->flush_ctx[std::make_pair(f->device, f->schema)];  // only this thread touches the map's values
+      if (!c) {
+        const SchemaParams *sp = nullptr;
+        for (const auto &x : config_.schemas)
+          if (x.schema_type == f->schema) sp = &x;
+        if (!sp) throw std::runtime_error("no parameters for schema " + std::to_string(f->schema));
+        fhe_params p = sp->params;
+        p.moduli = sp->moduli.empty() ? nullptr : sp->moduli.data();
+        if (fhe_ctx_create(&p, f->device, &c) != FHE_OK)
+          throw std::runtime_error(std::string("flusher fhe_ctx_create: ") + fhe_last_error(nullptr));
+        ck(c, fhe_use_own_stream(c), "flusher stream");
+      }
+      PartitionWriter out(f->file, f->durable);
+      const uint64_t row_bytes = 4 + sizeof(CtHeader) + f->cw * 8;
+      const size_t chunks = (f->rows + kRows - 1) / kRows;
+      const auto enqueue = [&](size_t ci) {
+        const size_t r0 = ci * kRows, n = std::min(kRows, f->rows - r0);
+        uint8_t *h = stage[ci & 1].reserve(c, kRows * f->cw * 8);
+        ck(c, fhe_memcpy_d2h_async(c, h, f->p + r0 * f->cw, n * f->cw * 8), "flush d2h");
+        ck(c, fhe_mark(c, (uint32_t)(ci & 1)), "flush mark");
+      };
+      if (chunks) enqueue(0);
+      for (size_t ci = 0; ci < chunks; ++ci) {
+        ck(c, fhe_wait_mark(c, (uint32_t)(ci & 1)), "flush wait");
+        if (ci + 1 < chunks) enqueue(ci + 1);
+        const size_t r0 = ci * kRows, n = std::min(kRows, f->rows - r0);
+        const uint64_t *host = reinterpret_cast<const uint64_t *>(stage[ci & 1].p);
+        const uint64_t base = out.claim(row_bytes * n);
+        parallel_for(n, config_.io_threads, [&](size_t r) {
+          out.write_row_at(base + r * row_bytes, {{&f->header, sizeof(CtHeader)}, {host + r * f->cw, f->cw * 8}});
+        });
+      }
+      out.commit();
+    } catch (const std::exception &e) {
+      err = e.what();
+    }
+    {
+      std::lock_guard lk(frames_->m);
+      auto it = frames_->pending.find(f->key);
+      if (it != frames_->pending.end() && it->second == f) frames_->pending.erase(it);
+      frames_->st.flush_s += secs_since(t0);
+      if (err.empty()) {
+        frames_->st.flushed_rows += f->rows;
+      } else {
+        frames_->failed = true;
+        std::fprintf(stderr, "GpuWorkerGroup: write-behind of %s failed: %s\n", f->file.c_str(), err.c_str());
+      }
+    }
+    frames_->cv.notify_all();
+  }
+}
 
 void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
   while (true) {
@@ -945,23 +1267,100 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         const std::vector<Instr> prog = lower_circuit(t.circuit);
         LaneSchema &ls = lane_schema(lane.schemas, config_, dev.id, schema);
         cur = &ls;
-        auto ks = device_keys(dev.keys_m, dev.keys, ls.s, config_.key_dir, t.session_uuid.as_string(), schema);
-        const PartitionIndex rows(frame_path(config_.storage_dir, t.session_uuid, t.input_data_frame_ptr.pointer));
-        PartitionWriter out(frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr),
-                            config_.durable_outputs);
+        const SchemaCtx &s = ls.s;
+        auto ks = device_keys(dev.keys_m, dev.keys, s, config_.key_dir, t.session_uuid.as_string(), schema);
+        const std::string in_key = frame_key(t.session_uuid, t.input_data_frame_ptr.pointer);
+        const std::string out_key = frame_key(t.session_uuid, t.output_data_frame_ptr);
+        const auto out_path = frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr);
+        std::vector<std::shared_ptr<ResidentFrame>> released;  // freed outside the frames lock
+        frames_->drop(out_key, released);  // the output partition is rewritten: no stale copy stays
+        MapIo io;
+        std::unique_ptr<PartitionIndex> in_file;
+        io.in = frames_->lookup(dev.id, in_key, schema);
+        if (!io.in) {
+          frames_->wait_file(in_key);  // a file still being written behind
+          in_file = std::make_unique<PartitionIndex>(
+              frame_path(config_.storage_dir, t.session_uuid, t.input_data_frame_ptr.pointer));
+          io.rows = in_file.get();
+        }
+        const size_t nrows = io.row_count();
+        // keep the output resident when every batch's result has one level
+        if (config_.resident_frame_bytes && nrows) {
+          uint32_t lvl = 0;
+          bool one = true;
+          std::vector<size_t> off;
+          std::vector<uint32_t> lv;
+          for (size_t r0 = 0; r0 < nrows && one; r0 += config_.max_batch) {
+            input_layout(s, io, max_input(prog), r0, off, lv);
+            const uint32_t l = program_level(prog, lv);
+            one = l != 0 && (r0 == 0 || l == lvl);
+            lvl = l;
+          }
+          const size_t cw = s.ct_words(lvl);
+          FrameBudget *budget = nullptr;
+          if (one) budget = frames_->reserve(dev.id, (uint64_t)nrows * cw * 8, config_.resident_frame_bytes, released);
+          if (budget) {
+            auto f = std::make_shared<ResidentFrame>();
+            f->key = out_key;
+            f->device = dev.id;
+            f->schema = schema;
+            f->level = lvl;
+            f->rows = nrows;
+            f->cw = cw;
+            f->ctx = s.ctx;
+            f->budget = budget;
+            f->file = out_path;
+            f->header = ct_header(s, lvl);
+            f->durable = config_.durable_outputs;
+            void *q = nullptr;
+            if (fhe_dev_alloc(s.ctx, f->bytes(), &q) == FHE_OK) {
+              f->p = static_cast<uint64_t *>(q);
+              io.out = std::move(f);
+            } else {
+              unreserve(frames_->m, *f->budget, *f);  // no room in HBM: the file path alone
+            }
+          }
+        }
+        released.clear();
+        io.write_file = !(config_.write_behind && io.out);
+        struct Unreserve {  // a failed task's resident output never reaches the map
+          Frames &fr;
+          std::shared_ptr<ResidentFrame> &f;
+          ~Unreserve() {
+            if (!f) return;
+            (void)fhe_synchronize(f->ctx);  // no copy into it is still in flight when it is freed
+            if (f->budget) unreserve(fr.m, *f->budget, *f);
+          }
+        } unreserve_on_failure{*frames_, io.out};
+        std::unique_ptr<PartitionWriter> out;
+        if (io.write_file) out = std::make_unique<PartitionWriter>(out_path, config_.durable_outputs);
         // two-deep software pipeline over the batches: enqueue batch k, then
         // write batch k-1 while batch k runs on the GPU, then read batch k+1
         int pending = -1;  // slot of the batch enqueued but not yet written
         size_t k = 0;
-        for (size_t r0 = 0; r0 < rows.size(); r0 += config_.max_batch, ++k) {
-          const size_t n = std::min<size_t>(config_.max_batch, rows.size() - r0);
+        for (size_t r0 = 0; r0 < nrows; r0 += config_.max_batch, ++k) {
+          const size_t n = std::min<size_t>(config_.max_batch, nrows - r0);
           const int si = (int)(k & 1);
-          enqueue_map_batch(ls, si, *ks, prog, rows, r0, n, config_.io_threads, stats);
-          if (pending >= 0) finish_map_batch(ls, pending, out, config_.io_threads, stats);
+          enqueue_map_batch(ls, si, *ks, prog, io, r0, n, config_.io_threads, stats);
+          if (pending >= 0) finish_map_batch(ls, pending, out.get(), config_.io_threads, stats);
           pending = si;
         }
-        if (pending >= 0) finish_map_batch(ls, pending, out, config_.io_threads, stats);
-        out.commit();
+        if (pending >= 0) finish_map_batch(ls, pending, out.get(), config_.io_threads, stats);
+        if (out) out->commit();
+        if (io.out) {
+          // every batch's copy into the frame has completed (the last mark);
+          // from here a task on any lane of this device reads it from HBM
+          frames_->publish(io.out, released);
+          if (!io.write_file) {
+            {
+              std::lock_guard lk(frames_->m);
+              frames_->pending[out_key] = io.out;
+              frames_->queue.push_back(io.out);
+            }
+            frames_->cv.notify_all();
+          }
+          io.out.reset();
+        }
       } else {
         // ReduceTask: combine every row of every input partition into one
         // ciphertext with a balanced tree of batched ADDs (MUL_RELIN if the
@@ -975,20 +1374,42 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         const bool mul = !prog.empty() && prog.front().op == Op::MUL_RELIN;
         std::shared_ptr<KeySet> ks;
         if (mul) ks = device_keys(dev.keys_m, dev.keys, s, config_.key_dir, t.session_uuid.as_string(), schema);
-        std::vector<std::unique_ptr<PartitionIndex>> parts;
+        {
+          std::vector<std::shared_ptr<ResidentFrame>> released;
+          frames_->drop(frame_key(t.session_uuid, t.output_data_frame_ptr), released);
+        }
+        // each input partition from HBM when a Map stage on this device left it
+        // resident, else from its file
+        struct Input {
+          std::unique_ptr<PartitionIndex> file;
+          std::shared_ptr<ResidentFrame> res;
+          size_t size() const { return res ? res->rows : file->size(); }
+        };
+        std::vector<Input> parts;
         size_t count = 0;
         for (const auto &in : t.input_data_frame_ptrs) {
-          parts.push_back(std::make_unique<PartitionIndex>(frame_path(config_.storage_dir, t.session_uuid, in.pointer)));
-          count += parts.back()->size();
+          Input pi;
+          const std::string key = frame_key(t.session_uuid, in.pointer);
+          pi.res = frames_->lookup(dev.id, key, schema);
+          if (!pi.res) {
+            frames_->wait_file(key);
+            pi.file = std::make_unique<PartitionIndex>(frame_path(config_.storage_dir, t.session_uuid, in.pointer));
+          }
+          count += pi.size();
+          parts.push_back(std::move(pi));
         }
         if (count == 0) throw std::runtime_error("reduce over no rows");
         // every row's first ciphertext, all at one level (the first row's)
         uint32_t level = 0;
         for (const auto &pv : parts)
-          if (pv->size()) {
-            CtHeader h;
-            pv->read(0, 0, &h, sizeof(h));
-            level = check_ct_header(s, h);
+          if (pv.size()) {
+            if (pv.res) {
+              level = pv.res->level;
+            } else {
+              CtHeader h;
+              pv.file->read(0, 0, &h, sizeof(h));
+              level = check_ct_header(s, h);
+            }
             break;
           }
         const size_t cw = s.ct_words(level);
@@ -1014,26 +1435,42 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         ArenaBuf stage[2] = {ArenaBuf(*ls.arena, C * cw), ArenaBuf(*ls.arena, C * cw)};
         bool used[2] = {false, false};
         size_t pi = 0, ri = 0, k = 0;
-        while (pi < parts.size() && parts[pi]->size() == 0) ++pi;
+        while (pi < parts.size() && parts[pi].size() == 0) ++pi;
         while (pi < parts.size()) {
           const int si = (int)(k++ & 1);
           Slot &sl = ls.slot[si];
           if (used[si]) ck(s.ctx, fhe_wait_mark(s.ctx, (uint32_t)si), "reduce slot wait");
           if (sl.in.empty()) sl.in.push_back(std::make_unique<Pinned>());
           uint64_t *host = reinterpret_cast<uint64_t *>(sl.in[0]->reserve(s.ctx, C * cw * 8));
-          size_t m = 0;
+          // the chunk's rows in partition order (the same tree whatever is
+          // resident): file rows staged through pinned memory, resident rows
+          // copied on the device
+          size_t m = 0, h0 = 0;  // h0: first chunk row of the current host run
+          const auto flush_host = [&](size_t upto) {
+            if (upto > h0)
+              ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, stage[si].p + h0 * cw, host + h0 * cw, (upto - h0) * cw * 8), "h2d");
+          };
           for (; m < C && pi < parts.size(); ++m) {
-            CtHeader h;
-            parts[pi]->read(ri, 0, &h, sizeof(h));
-            if (check_ct_header(s, h) != level) throw std::runtime_error("reduce inputs differ in ciphertext level");
-            parts[pi]->read(ri, sizeof(h), host + m * cw, cw * 8);
-            if (++ri == parts[pi]->size()) {
+            Input &in = parts[pi];
+            if (in.res) {
+              if (in.res->level != level) throw std::runtime_error("reduce inputs differ in ciphertext level");
+              flush_host(m);
+              h0 = m + 1;
+              ck(s.ctx, fhe_memcpy_d2d_async(s.ctx, stage[si].p + m * cw, in.res->p + ri * in.res->cw, cw * 8), "d2d");
+              stats.resident_rows += 1;
+            } else {
+              CtHeader h;
+              in.file->read(ri, 0, &h, sizeof(h));
+              if (check_ct_header(s, h) != level) throw std::runtime_error("reduce inputs differ in ciphertext level");
+              in.file->read(ri, sizeof(h), host + m * cw, cw * 8);
+            }
+            if (++ri == in.size()) {
               ri = 0;
               ++pi;
-              while (pi < parts.size() && parts[pi]->size() == 0) ++pi;
+              while (pi < parts.size() && parts[pi].size() == 0) ++pi;
             }
           }
-          ck(s.ctx, fhe_memcpy_h2d_async(s.ctx, stage[si].p, host, m * cw * 8), "h2d");
+          flush_host(m);
           ck(s.ctx, fhe_mark(s.ctx, (uint32_t)si), "reduce slot mark");
           used[si] = true;
           Partial p{ArenaBuf(*ls.arena, cw), 0};

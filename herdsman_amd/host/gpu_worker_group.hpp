@@ -69,6 +69,9 @@ struct StageStats {
   double read_s = 0, enqueue_s = 0, wait_s = 0, write_s = 0;
   double task_s = 0;  // whole tasks on the lanes, open to commit
   uint64_t batches = 0, rows = 0, tasks = 0;
+  uint64_t resident_rows = 0;   // input rows read from a frame kept in HBM (no pread, no H2D)
+  uint64_t flushed_rows = 0;    // rows the write-behind flusher wrote to partition files
+  double flush_s = 0;           // the flusher's time (D2H + file writes), off the lanes
   StageStats &operator+=(const StageStats &o) {
     task_s += o.task_s;
     tasks += o.tasks;
@@ -78,6 +81,9 @@ struct StageStats {
     write_s += o.write_s;
     batches += o.batches;
     rows += o.rows;
+    resident_rows += o.resident_rows;
+    flushed_rows += o.flushed_rows;
+    flush_s += o.flush_s;
     return *this;
   }
 };
@@ -91,6 +97,20 @@ struct GpuWorkerGroupConfig {
   uint32_t max_batch = 64;            // rows per batched GPU call
   bool durable_outputs = false;       // fsync output partitions (PartitionWriter)
   uint32_t io_threads = 4;            // threads per lane reading / writing a batch's rows
+  // Resident frames: every MapTask output partition (one ciphertext per row, one
+  // level) also stays in HBM, per device, least recently used first out, at most
+  // this many bytes per device (0: off).  A MapTask or ReduceTask on the same
+  // device whose input partition is resident reads it from HBM: no pread, no H2D.
+  // herdsman chains Map stages through intermediate-<job>-<node> frames that the
+  // next stage reads back (execution_service.cpp:525-543), which is the case this
+  // serves.  The partition file is still written (the storage contract holds).
+  uint64_t resident_frame_bytes = 16ull << 30;
+  // write_behind: a MapTask whose output is resident completes once that output
+  // is in HBM, and the group's flusher thread writes the partition file behind
+  // it (D2H + file writes off the lanes).  flush_frames() returns once every
+  // file is committed; a task that must read a file still being flushed waits
+  // for it.  Off by default: then a task completes after its file is committed.
+  bool write_behind = false;
 };
 
 class GpuWorkerGroup : public IWorkerGroup {
@@ -103,6 +123,9 @@ class GpuWorkerGroup : public IWorkerGroup {
   // summed over the lanes since construction / the last reset (not part of the seam)
   StageStats stage_stats();
   void reset_stage_stats();
+  // write_behind: block until every partition file queued so far is committed;
+  // false if a flush failed (its message on stderr).  No-op otherwise.
+  bool flush_frames();
   // false when herd_common's Circuit has no lowering to the backend's ops
   // (under HERDSMAN_REAL_SEAM): the group then fails every task at once
   static bool circuits_lowerable() noexcept;
@@ -113,9 +136,11 @@ class GpuWorkerGroup : public IWorkerGroup {
   struct Job;
   struct Device;
   struct Lane;
+  struct Frames;
 
   void lane_loop(Device &dev, Lane &lane);
   void completion_loop();
+  void flush_loop();
   void complete(const std::shared_ptr<Handle> &h, TaskHandle::Status st);
 
   GpuWorkerGroupConfig config_;
@@ -129,6 +154,8 @@ class GpuWorkerGroup : public IWorkerGroup {
   std::thread completion_thread_;
   std::mutex stats_m_;
   StageStats stats_;
+  std::unique_ptr<Frames> frames_;  // resident frames and the write-behind flusher
+  std::thread flush_thread_;
 };
 
 class GpuWorkerGroup::Handle : public IWorkerGroup::TaskHandle {

@@ -6,6 +6,9 @@
 //   wg_run map    STORAGE KEYS SESSION SCHEMA PARAMS IN_FRAME PART OUT_FRAME PROGRAM...
 //   wg_run reduce STORAGE KEYS SESSION SCHEMA PARAMS OUT_FRAME OUT_PART IN_FRAME:PART... [-- mul]
 //   wg_run race   N            (seam test: N malformed tasks, callback attached late)
+//   wg_run chain  STORAGE KEYS SESSION SCHEMA PARAMS IN_FRAME PARTS MID_FRAME OUT_FRAME PROG1... -- PROG2...
+//                 two chained Map stages over PARTS partitions (stage 2 reads stage 1's
+//                 output frame, from HBM when it is resident)
 //   wg_run bench  DIR PARAMS PARTS ROWS [LANES [MAX_BATCH [REPS]]]
 //                 MapTask throughput: writes PARTS partitions of ROWS rows
 //                 (two ciphertexts each, uniform residues made on the GPU) and a
@@ -15,6 +18,12 @@
 //                 (partition read, PCIe both ways, GPU, partition write): the
 //                 mean and spread of REPS (default 5) warm repetitions after one
 //                 warm-up, and where the lanes' time went (GpuWorkerGroup::stage_stats).
+//   wg_run chainbench DIR PARAMS PARTS ROWS [LANES [MAX_BATCH [REPS]]]
+//                 the same inputs; stage 1 "in0 in1 mul" into a fresh frame, then stage 2
+//                 "in0 in0 mul" over that frame, each timed (stage 2 with and without
+//                 waiting for write-behind files)
+// Group knobs from the environment: WG_DEVICE, WG_LANES, WG_MAX_BATCH, WG_IO_THREADS,
+// WG_RESIDENT_BYTES (0 = no resident frames), WG_WRITE_BEHIND=1
 // PARAMS = scheme,log_n,L,K,dnum,t[,moduli_file[,behz|hps]]   PROGRAM tokens: in<i> add sub mul rot:<k> rescale
 #include <algorithm>
 #include <chrono>
@@ -117,8 +126,70 @@ static void ckb(fhe_ctx *c, int rc, const char *what) {
   if (rc != FHE_OK) throw std::runtime_error(std::string(what) + ": " + fhe_last_error(c));
 }
 
+// group knobs from the environment (every mode): WG_DEVICE, WG_LANES, WG_MAX_BATCH,
+// WG_IO_THREADS, WG_RESIDENT_BYTES (0: no resident frames), WG_WRITE_BEHIND=1
+static void env_config(GpuWorkerGroupConfig &cfg) {
+  if (const char *d = std::getenv("WG_DEVICE")) cfg.devices = {std::atoi(d)};
+  if (const char *v = std::getenv("WG_LANES")) cfg.lanes_per_device = (uint32_t)std::atoi(v);
+  if (const char *v = std::getenv("WG_MAX_BATCH")) cfg.max_batch = (uint32_t)std::atoi(v);
+  if (const char *t = std::getenv("WG_IO_THREADS")) cfg.io_threads = (uint32_t)std::max(1, std::atoi(t));
+  if (const char *v = std::getenv("WG_RESIDENT_BYTES")) cfg.resident_frame_bytes = std::strtoull(v, nullptr, 10);
+  if (const char *v = std::getenv("WG_WRITE_BEHIND")) cfg.write_behind = v[0] == '1';
+}
+
+// Keep concurrent_workers() tasks in flight, as the Executor does
+// (executor.cpp:96-113); returns the wall time until the last completion.
+template <class Make>
+static double run_all(GpuWorkerGroup &g, int count, Make make) {
+  std::mutex m;
+  std::condition_variable cv;
+  int done = 0, errors = 0, next = 0, inflight = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::unique_lock lk(m);
+  while (done < count) {
+    while (next < count && inflight < (int)g.concurrent_workers()) {
+      lk.unlock();
+      auto h = g.schedule_task(make(next));
+      h->set_completion_callback([&](Status s) {
+        std::lock_guard l2(m);
+        ++done;
+        --inflight;
+        if (s != Status::COMPLETED) ++errors;
+        cv.notify_one();
+      });
+      lk.lock();
+      ++next;
+      ++inflight;
+    }
+    cv.wait(lk);
+  }
+  if (errors) throw std::runtime_error("tasks failed");
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+static void print_stages(const herdsman_gpu::StageStats &st) {
+  const double lane_s = st.read_s + st.enqueue_s + st.wait_s + st.write_s;
+  std::printf("stages (summed over lanes, warm reps): %llu tasks, %llu batches, %llu rows (%llu read from HBM-resident "
+              "frames); task time %.3f s (%.1f ms per task, of which the stages below %.1f ms)\n",
+              (unsigned long long)st.tasks, (unsigned long long)st.batches, (unsigned long long)st.rows,
+              (unsigned long long)st.resident_rows, st.task_s, st.tasks ? 1e3 * st.task_s / st.tasks : 0.0,
+              st.tasks ? 1e3 * lane_s / st.tasks : 0.0);
+  const std::pair<const char *, double> rowsv[] = {{"read rows -> pinned (pread)", st.read_s},
+                                                   {"enqueue H2D + kernels + D2H", st.enqueue_s},
+                                                   {"wait for the batch's GPU work", st.wait_s},
+                                                   {"write output rows", st.write_s}};
+  for (const auto &r : rowsv)
+    std::printf("  %-32s %8.3f s  %5.1f%%  %8.2f ms/batch\n", r.first, r.second, lane_s > 0 ? 100 * r.second / lane_s : 0.0,
+                st.batches ? 1e3 * r.second / st.batches : 0.0);
+  if (st.flushed_rows)
+    std::printf("  write-behind flusher (off the lanes): %llu rows in %.3f s\n", (unsigned long long)st.flushed_rows,
+                st.flush_s);
+}
+
 static int bench(int argc, char **argv) {
-  if (argc < 6) throw std::runtime_error("usage: wg_run bench DIR PARAMS PARTS ROWS [LANES [MAX_BATCH [REPS]]]");
+  const std::string mode = argv[1];
+  if (argc < 6)
+    throw std::runtime_error("usage: wg_run bench|chainbench DIR PARAMS PARTS ROWS [LANES [MAX_BATCH [REPS]]]");
   const std::filesystem::path dir = argv[2];
   const herdsman_gpu::SchemaParams sp = parse_params(0, argv[3]);
   const int parts = std::atoi(argv[4]), rows = std::atoi(argv[5]);
@@ -129,8 +200,7 @@ static int bench(int argc, char **argv) {
   if (argc > 6) cfg.lanes_per_device = (uint32_t)std::atoi(argv[6]);
   if (argc > 7) cfg.max_batch = (uint32_t)std::atoi(argv[7]);
   const int reps = argc > 8 ? std::max(1, std::atoi(argv[8])) : 5;
-  if (const char *t = std::getenv("WG_IO_THREADS")) cfg.io_threads = (uint32_t)std::max(1, std::atoi(t));
-  if (const char *d = std::getenv("WG_DEVICE")) cfg.devices = {std::atoi(d)};
+  env_config(cfg);
   // ---- synthetic inputs, made on the device with the backend's uniform fill
   fhe_params p = sp.params;
   p.moduli = sp.moduli.empty() ? nullptr : sp.moduli.data();
@@ -186,75 +256,76 @@ static int bench(int argc, char **argv) {
   fhe_dev_free(c, dbuf);
   fhe_ctx_destroy(c);
   // ---- the Executor's pattern: keep concurrent_workers() tasks in flight
-  herd::common::Circuit circ;
-  circ.program = {{herd::common::CtOp::PUSH_INPUT, 0}, {herd::common::CtOp::PUSH_INPUT, 1},
-                  {herd::common::CtOp::MUL_RELIN, 0}};
-  int rep_no = 0;  // each repetition writes a fresh output frame, as every herdsman job does
-  auto make = [&](int part) {
+  using herd::common::CtOp;
+  herd::common::Circuit mul2, sq;
+  mul2.program = {{CtOp::PUSH_INPUT, 0}, {CtOp::PUSH_INPUT, 1}, {CtOp::MUL_RELIN, 0}};
+  sq.program = {{CtOp::PUSH_INPUT, 0}, {CtOp::PUSH_INPUT, 0}, {CtOp::MUL_RELIN, 0}};
+  auto task = [&](const std::string &in, const std::string &out, int part, const herd::common::Circuit &c) {
     herd::common::MapTask t;
     t.session_uuid = {"bench"};
-    t.input_data_frame_ptr.pointer = {{"in"}, (uint32_t)part};
+    t.input_data_frame_ptr.pointer = {{in}, (uint32_t)part};
     t.input_data_frame_ptr.row_count = (uint64_t)rows;
-    t.output_data_frame_ptr = {{"out" + std::to_string(rep_no)}, (uint32_t)part};
+    t.output_data_frame_ptr = {{out}, (uint32_t)part};
     t.crypto_key_ptr.schema_type = herd::common::SchemaType::CKKS;
-    t.circuit = circ;
+    t.circuit = c;
     return herd::common::task_t{t};
   };
-  std::vector<double> rates;
+  const bool chain = mode == "chainbench";
+  std::vector<double> rates, rates2, rates2f;
   GpuWorkerGroup g(cfg);  // one long-lived group, as in a server
+  herdsman_gpu::StageStats st1;
   for (int rep = 0; rep <= reps; ++rep) {  // rep 0 warms contexts, keys, pinned and device buffers
-    if (rep == 1) g.reset_stage_stats();
-    rep_no = rep;
-    if (rep > 0) std::filesystem::remove_all(cfg.storage_dir / "bench" / ("out" + std::to_string(rep - 1)));
-    std::mutex m;
-    std::condition_variable cv;
-    int done = 0, errors = 0, next = 0, inflight = 0;
-    const auto t0 = std::chrono::steady_clock::now();
-    std::unique_lock lk(m);
-    while (done < parts) {
-      while (next < parts && inflight < (int)g.concurrent_workers()) {
-        lk.unlock();
-        auto h = g.schedule_task(make(next));
-        h->set_completion_callback([&](Status s) {
-          std::lock_guard l2(m);
-          ++done;
-          --inflight;
-          if (s != Status::COMPLETED) ++errors;
-          cv.notify_one();
-        });
-        lk.lock();
-        ++next;
-        ++inflight;
-      }
-      cv.wait(lk);
+    // each repetition writes fresh output frames, as every herdsman job does
+    const std::string mid = "out" + std::to_string(rep), fin = "fin" + std::to_string(rep);
+    if (rep > 0) {
+      std::filesystem::remove_all(cfg.storage_dir / "bench" / ("out" + std::to_string(rep - 1)));
+      std::filesystem::remove_all(cfg.storage_dir / "bench" / ("fin" + std::to_string(rep - 1)));
     }
-    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (errors) throw std::runtime_error("bench tasks failed");
+    if (rep == 1) g.reset_stage_stats();
+    // stage 1: "in0 in1 mul" over the input partitions (files)
+    const double dt = run_all(g, parts, [&](int p) { return task("in", mid, p, mul2); });
     const double rate = (double)parts * rows / dt;
-    std::printf("bench rep %d: %d MapTasks x %d rows in %.3f s = %.1f ct-mult+relin/s (%zu workers)\n", rep, parts,
-                rows, dt, rate, g.concurrent_workers());
+    std::printf("%s rep %d: %d MapTasks x %d rows in %.3f s = %.1f ct-mult+relin/s (%zu workers)\n",
+                chain ? "stage-1" : "bench", rep, parts, rows, dt, rate, g.concurrent_workers());
     if (rep) rates.push_back(rate);
+    if (!chain) continue;
+    if (!g.flush_frames()) throw std::runtime_error("write-behind failed");  // stage 1's files, off the clock
+    if (rep) {
+      herdsman_gpu::StageStats a = g.stage_stats();
+      st1 += a;
+      g.reset_stage_stats();
+    }
+    // stage 2: "in0 in0 mul" over stage 1's output frame (intermediate-<job>-<node>
+    // in herdsman), read from HBM when resident; then every file committed
+    const double dt2 = run_all(g, parts, [&](int p) { return task(mid, fin, p, sq); });
+    const auto t1 = std::chrono::steady_clock::now();
+    if (!g.flush_frames()) throw std::runtime_error("write-behind failed");
+    const double dtf = dt2 + std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    std::printf("stage-2 rep %d: %d MapTasks x %d rows in %.3f s = %.1f ct-mult+relin/s; with every file committed "
+                "%.3f s = %.1f/s\n", rep, parts, rows, dt2, parts * rows / dt2, dtf, parts * rows / dtf);
+    if (rep) {
+      rates2.push_back(parts * rows / dt2);
+      rates2f.push_back(parts * rows / dtf);
+    }
   }
-  double mean = 0;
-  for (double r : rates) mean += r / rates.size();
-  const auto mm = std::minmax_element(rates.begin(), rates.end());
-  std::printf("bench: %.1f ct-mult+relin/s mean of %zu warm reps (min %.1f, max %.1f); %d partitions x %d rows, "
-              "max_batch %u, %zu lanes, %u io threads per lane\n",
-              mean, rates.size(), *mm.first, *mm.second, parts, rows, cfg.max_batch, g.concurrent_workers(),
-              cfg.io_threads);
-  const herdsman_gpu::StageStats st = g.stage_stats();
-  const double lane_s = st.read_s + st.enqueue_s + st.wait_s + st.write_s;
-  std::printf("stages (summed over lanes, warm reps): %llu tasks, %llu batches, %llu rows; task time %.3f s "
-              "(%.1f ms per task, of which the stages below %.1f ms)\n",
-              (unsigned long long)st.tasks, (unsigned long long)st.batches, (unsigned long long)st.rows, st.task_s,
-              st.tasks ? 1e3 * st.task_s / st.tasks : 0.0, st.tasks ? 1e3 * lane_s / st.tasks : 0.0);
-  const std::pair<const char *, double> rowsv[] = {{"read rows -> pinned (pread)", st.read_s},
-                                                   {"enqueue H2D + kernels + D2H", st.enqueue_s},
-                                                   {"wait for the batch's GPU work", st.wait_s},
-                                                   {"write output rows", st.write_s}};
-  for (const auto &r : rowsv)
-    std::printf("  %-32s %8.3f s  %5.1f%%  %8.2f ms/batch\n", r.first, r.second, 100 * r.second / lane_s,
-                st.batches ? 1e3 * r.second / st.batches : 0.0);
+  auto summary = [&](const char *what, const std::vector<double> &v) {
+    double mean = 0;
+    for (double r : v) mean += r / v.size();
+    const auto mm = std::minmax_element(v.begin(), v.end());
+    std::printf("%s: %.1f ct-mult+relin/s mean of %zu warm reps (min %.1f, max %.1f); %d partitions x %d rows, "
+                "max_batch %u, %zu lanes, %u io threads per lane, resident frames %s, write-behind %s\n",
+                what, mean, v.size(), *mm.first, *mm.second, parts, rows, cfg.max_batch, g.concurrent_workers(),
+                cfg.io_threads, cfg.resident_frame_bytes ? "on" : "off", cfg.write_behind ? "on" : "off");
+  };
+  summary(chain ? "stage-1" : "bench", rates);
+  if (chain) {
+    summary("stage-2 (tasks complete)", rates2);
+    summary("stage-2 (files committed)", rates2f);
+    std::printf("stage 1:\n");
+    print_stages(st1);
+    std::printf("stage 2:\n");
+  }
+  print_stages(g.stage_stats());
   return 0;
 }
 
@@ -275,7 +346,7 @@ int main(int argc, char **argv) {
       std::printf("race: %d/%d delivered, concurrent_workers=%zu\n", delivered, n, g.concurrent_workers());
       return delivered == n ? 0 : 1;
     }
-    if (mode == "bench") return bench(argc, argv);
+    if (mode == "bench" || mode == "chainbench") return bench(argc, argv);
     if (argc < 8) throw std::runtime_error("missing arguments");
     GpuWorkerGroupConfig cfg;
     cfg.storage_dir = argv[2];
@@ -283,11 +354,58 @@ int main(int argc, char **argv) {
     const std::string session = argv[4];
     const int schema = std::atoi(argv[5]);
     cfg.schemas = {parse_params(schema, argv[6])};
-    if (const char *d = std::getenv("WG_DEVICE")) cfg.devices = {std::atoi(d)};
-    if (const char *v = std::getenv("WG_LANES")) cfg.lanes_per_device = (uint32_t)std::atoi(v);
-    if (const char *v = std::getenv("WG_MAX_BATCH")) cfg.max_batch = (uint32_t)std::atoi(v);
+    env_config(cfg);
     GpuWorkerGroup g(cfg);
     Status st;
+    if (mode == "chain") {
+      // herdsman's chained Map stages: stage 1 over every partition of IN_FRAME
+      // into MID_FRAME, then (once all of stage 1 completed, as the
+      // ExecutionService schedules the next stage) stage 2 over MID_FRAME into
+      // OUT_FRAME, on the same group; then every file committed
+      if (argc < 11) throw std::runtime_error("usage: wg_run chain ... IN_FRAME PARTS MID_FRAME OUT_FRAME PROG1 -- PROG2");
+      const int parts = std::atoi(argv[8]);
+      int sep = 11;
+      while (sep < argc && std::string(argv[sep]) != "--") ++sep;
+      if (sep >= argc) throw std::runtime_error("chain: PROG1 -- PROG2");
+      // PROG2 "reduce [mul]": one ReduceTask over every partition of MID_FRAME into OUT_FRAME:0
+      const bool reduce2 = sep + 1 < argc && std::string(argv[sep + 1]) == "reduce";
+      const herd::common::Circuit c1 = parse_program(sep, argv, 11);
+      const herd::common::Circuit c2 = reduce2 ? herd::common::Circuit{} : parse_program(argc, argv, sep + 1);
+      auto make = [&](const char *in, const char *out, const herd::common::Circuit &c) {
+        return [&, in, out](int p) {
+          herd::common::MapTask t;
+          t.session_uuid = {session};
+          t.input_data_frame_ptr.pointer = {{in}, (uint32_t)p};
+          t.output_data_frame_ptr = {{out}, (uint32_t)p};
+          t.crypto_key_ptr.schema_type = static_cast<herd::common::SchemaType>(schema);
+          t.circuit = c;
+          return herd::common::task_t{t};
+        };
+      };
+      run_all(g, parts, make(argv[7], argv[9], c1));
+      if (reduce2) {
+        herd::common::ReduceTask t;
+        t.session_uuid = {session};
+        t.output_data_frame_ptr = {{argv[10]}, 0};
+        t.crypto_key_ptr.schema_type = static_cast<herd::common::SchemaType>(schema);
+        if (sep + 2 < argc && std::string(argv[sep + 2]) == "mul")
+          t.circuit.program.push_back({herd::common::CtOp::MUL_RELIN, 0});
+        for (int p = 0; p < parts; ++p) {
+          herd::common::InputDataFramePtr in;
+          in.pointer = {{argv[9]}, (uint32_t)p};
+          t.input_data_frame_ptrs.push_back(in);
+        }
+        if (run(g, t) != Status::COMPLETED) throw std::runtime_error("reduce stage failed");
+      } else {
+        run_all(g, parts, make(argv[9], argv[10], c2));
+      }
+      const bool flushed = g.flush_frames();
+      const herdsman_gpu::StageStats ss = g.stage_stats();
+      std::printf("chain: rows %llu resident_rows %llu flushed_rows %llu\n", (unsigned long long)ss.rows,
+                  (unsigned long long)ss.resident_rows, (unsigned long long)ss.flushed_rows);
+      std::printf("status: %s\n", flushed ? "COMPLETED" : "ERROR");
+      return flushed ? 0 : 2;
+    }
     if (mode == "map") {
       // PART may list several partitions ("1,0"): one MapTask each, in order, on
       // the same group (a failed task must leave its lane usable for the next)

@@ -102,6 +102,9 @@ int fhe_host_alloc(fhe_ctx *ctx, size_t bytes, void **out);
 int fhe_host_free(fhe_ctx *ctx, void *ptr);
 int fhe_memcpy_h2d_async(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
 int fhe_memcpy_d2h_async(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* device-to-device copy enqueued on the context's stream (the worker group
+ * keeps a MapTask's output frame resident in HBM for the stage that reads it) */
+int fhe_memcpy_d2d_async(fhe_ctx *ctx, void *dst, const void *src, size_t bytes);
 /* give the context a HIP stream of its own (non-blocking, destroyed with the
  * context) for callers without a stream of their own: several contexts on one
  * device then run concurrently, e.g. the worker group's lanes */
@@ -159,7 +162,7 @@ int fhe_rotate_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const u
  * Q u P before ONE ModDown (the hoisted-ModDown baby-step sum of linear
  * transforms).  Decrypts to the sum of the rotated messages; the bits differ
  * from adding fhe_rotate_hoisted's outputs by the ModDown rounding (oracle
- * orc_rotate_sum_hoisted_at).  galois_elts, gks: HOST arrays; out may alias ct. */
+ * orc_rotate_sum_hoisted_at).  galois_elts, gks: HOST arrays; out may be ct itself (in place) or apart from it; a partial overlap is FHE_ERR_INVALID. */
 int fhe_rotate_sum_hoisted(fhe_ctx *ctx, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois_elts,
                            const uint64_t *const *gks, uint64_t *out, uint32_t n_ct);
 /* hoisted linear transform (CKKS; the baby-step block of a matrix-vector

@@ -213,6 +213,18 @@ def test_rotation_sum_double_hoisted(hb, scheme, log_n, L, K, dnum, n_ct, steps)
     assert np.array_equal(hb.to_host(io), want)
 
 
+def test_rotation_sum_partial_overlap_is_refused(hb):
+    """out == ct (in place) or apart; a partial overlap is FHE_ERR_INVALID (the
+    work runs in chunks, and a shifted out would overwrite rows a later chunk reads)."""
+    o = Oracle(SCHEME_CKKS, 12, 4, 2, 2)
+    c = hb.Context(SCHEME_CKKS, 12, 4, 2, 2, moduli=o.moduli)
+    buf = hb.empty((3, 2, 4, o.n))
+    gs = [o.galois_elt(1)]
+    d_gk = [hb.to_device(o.uniform(o.key_shape(), seed=1830))]
+    with pytest.raises(hb.FheBackendError, match="overlap"):
+        c.rotate_sum_hoisted(buf[:2], gs, d_gk, buf[1:])
+
+
 def test_rotation_sum_double_hoisted_at_level(hb, metric):
     o, c = metric
     lvl = 7

@@ -145,6 +145,11 @@ def test_level_argument_errors(hb, metric):
     rc = lib.fhe_mul_relin_at(bfv.h, hb._ptr(z), hb._ptr(z), hb._ptr(kz), hb._ptr(z), 1, 2)
     assert rc == hb.FHE_ERR_UNSUPPORTED
     assert lib.fhe_rescale(bfv.h, hb._ptr(z), hb._ptr(z), 1, 2) == hb.FHE_ERR_UNSUPPORTED
+    # BFV has no reduced levels: the element-wise ops refuse them too
+    assert lib.fhe_add_at(bfv.h, hb._ptr(z), hb._ptr(z), hb._ptr(z), 1, 2) == hb.FHE_ERR_UNSUPPORTED
+    assert lib.fhe_sub_at(bfv.h, hb._ptr(z), hb._ptr(z), hb._ptr(z), 1, 2) == hb.FHE_ERR_UNSUPPORTED
+    w = hb.empty((1, 2, 3, 1 << 12))
+    assert lib.fhe_add_at(bfv.h, hb._ptr(w), hb._ptr(w), hb._ptr(w), 1, 3) == hb.FHE_OK
 
 
 def _decrypt_at(o, ct, s_qp, lvl):

@@ -313,28 +313,39 @@ def test_gpu_reduce_task_chunked(wg_run, tmp_path):
                        timeout=600, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     got = parse_row(o, read_partition(os.path.join(storage, "s3", "outM", "0"))[0], level=lvl)
+    assert np.array_equal(got, _reduce_tree_chunked(o, cts, rlk, True, 2, lvl))
 
-    def mul(x, y):
-        return o.mul_relin_at(x[None], y[None], rlk, lvl)[0]
+
+def _reduce_tree_chunked(o, cts, rlk, mul, chunk, lvl=None):
+    """The worker group's ReduceTask tree: chunks of `chunk` rows in partition
+    order, each a balanced tree (fhe_reduce_at), the chunk results merged like a
+    binary counter (older operand first)."""
+    lvl = o.L if lvl is None else lvl
+    qs = o.moduli[:lvl].astype(object)[None, :, None]
+
+    def op(x, y):
+        if mul:
+            return o.mul_relin_at(x[None], y[None], rlk, lvl)[0]
+        return ((x.astype(object) + y) % qs).astype(np.uint64)
 
     def tree(items):
         live = list(items)
         while len(live) > 1:
             half = len(live) // 2
-            comb = [mul(live[j], live[len(live) - half + j]) for j in range(half)]
+            comb = [op(live[j], live[len(live) - half + j]) for j in range(half)]
             live = comb + live[half:len(live) - half]
         return live[0]
 
     pend = []
-    for c0 in range(0, len(cts), 2):
-        p, h = tree(cts[c0:c0 + 2]), 0
+    for c0 in range(0, len(cts), chunk):
+        p, h = tree(cts[c0:c0 + chunk]), 0
         while pend and pend[-1][1] == h:
-            p, h = mul(pend.pop()[0], p), h + 1
+            p, h = op(pend.pop()[0], p), h + 1
         pend.append((p, h))
     while len(pend) > 1:
         p = pend.pop()[0]
-        pend[-1] = (mul(pend[-1][0], p), pend[-1][1])
-    assert np.array_equal(got, pend[0][0])
+        pend[-1] = (op(pend[-1][0], p), pend[-1][1])
+    return pend[0][0]
 
 
 @pytest.mark.gpu
@@ -407,3 +418,83 @@ def test_gpu_failed_batch_leaves_the_lane_usable(wg_run, tmp_path):
     assert not os.path.exists(os.path.join(storage, "sl", "out", "1"))
     got = np.stack([parse_row(o, p) for p in read_partition(os.path.join(storage, "sl", "out", "0"))])
     assert np.array_equal(got, o.mul_relin(a, b, rlk))
+
+
+def _chain(wg_run, tmp_path, o, storage, keys, session, schema, parts, prog1, prog2, resident, write_behind):
+    env = dict(os.environ, WG_MAX_BATCH="2", WG_LANES="3", WG_RESIDENT_BYTES=str(resident),
+               WG_WRITE_BEHIND="1" if write_behind else "0")
+    r = subprocess.run([wg_run, "chain", storage, keys, session, str(schema), params_arg(o, str(tmp_path)), "fa",
+                        str(parts), "fm", "fo"] + prog1 + ["--"] + prog2,
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("chain:")][0].split()
+    return {line[i]: int(line[i + 1]) for i in range(1, len(line), 2)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("resident,write_behind", [(1 << 34, False), (1 << 34, True), (0, False),
+                                                   (3 * 2 * 4 * 4096 * 8 * 2, True)])
+def test_gpu_chained_map_stages_resident_frames(wg_run, tmp_path, resident, write_behind):
+    """herdsman chains Map stages through intermediate frames that the next stage
+    reads back (execution_service.cpp:525-543).  Stage 1 "in0 in1 mul rescale"
+    writes frame fm; stage 2 "in0 in0 mul rot:1" reads it.  With resident frames
+    stage 2 reads fm from HBM (no pread, no H2D; resident_rows counts them), with
+    write-behind fm's and fo's files are committed by the flusher; with no budget
+    everything goes through the files; with a budget of two partitions' frames
+    the third evicts the first (its stage-2 task then reads the file).  Both
+    frames' files are bit-exact against the oracle in every mode."""
+    from oracle_ffi import SCHEME_CKKS
+    o, storage, keys = _setup(tmp_path, SCHEME_CKKS, 12, 4, 2, 2)
+    parts, rows = 3, 5
+    a = o.uniform((parts, rows, 2, o.L, o.n), seed=91)
+    b = o.uniform((parts, rows, 2, o.L, o.n), seed=92)
+    rlk = o.uniform(o.key_shape(), seed=93)
+    g = o.galois_elt(1)
+    gk = o.uniform(o.key_shape(), seed=94)
+    for p in range(parts):
+        write_partition(os.path.join(storage, "sc", "fa", str(p)), [ct_row(o, [a[p, i], b[p, i]]) for i in range(rows)])
+    write_keys(os.path.join(keys, "sc", "0.key"), o, rlk, {g: gk})
+    st = _chain(wg_run, tmp_path, o, storage, keys, "sc", 0, parts, ["in0", "in1", "mul", "rescale"],
+                ["in0", "in0", "mul", "rot:1"], resident, write_behind)
+    for p in range(parts):
+        mid = o.rescale(o.mul_relin(a[p], b[p], rlk), o.L)
+        got_mid = np.stack([parse_row(o, r, level=o.L - 1) for r in read_partition(os.path.join(storage, "sc", "fm", str(p)))])
+        assert np.array_equal(got_mid, mid), p
+        fin = o.rotate_at(o.mul_relin_at(mid, mid, rlk, o.L - 1), g, gk, o.L - 1)
+        got = np.stack([parse_row(o, r, level=o.L - 1) for r in read_partition(os.path.join(storage, "sc", "fo", str(p)))])
+        assert np.array_equal(got, fin), p
+    assert st["rows"] == 2 * parts * rows
+    if resident >= 1 << 34:
+        assert st["resident_rows"] == parts * rows  # every stage-2 row came from HBM
+    elif resident == 0:
+        assert st["resident_rows"] == 0
+    else:
+        assert 0 < st["resident_rows"] < parts * rows  # the evicted partition was read from its file
+    assert st["flushed_rows"] == (2 * parts * rows if write_behind and resident >= 1 << 34 else st["flushed_rows"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mul", [False, True])
+def test_gpu_map_then_reduce_reads_resident_frames(wg_run, tmp_path, mul):
+    """A ReduceTask over a Map stage's output partitions reads them from HBM and
+    builds the same tree (chunks of max_batch rows across partitions) as from
+    files: bit-exact against the oracle's tree."""
+    from oracle_ffi import SCHEME_BFV
+    o, storage, keys = _setup(tmp_path, SCHEME_BFV, 12, 3, 3, 1, t=65537)
+    parts, rows = 3, 3
+    a = o.uniform((parts, rows, 2, o.L, o.n), seed=95)
+    b = o.uniform((parts, rows, 2, o.L, o.n), seed=96)
+    rlk = o.uniform(o.key_shape(), seed=97)
+    for p in range(parts):
+        write_partition(os.path.join(storage, "sd", "fa", str(p)), [ct_row(o, [a[p, i], b[p, i]]) for i in range(rows)])
+    write_keys(os.path.join(keys, "sd", "1.key"), o, rlk, {})
+    st = _chain(wg_run, tmp_path, o, storage, keys, "sd", 1, parts, ["in0", "in1", "add"],
+                ["reduce"] + (["mul"] if mul else []), 1 << 34, False)
+    assert st["resident_rows"] == parts * rows
+    mids = [((a[p].astype(object) + b[p]) % o.moduli[:o.L].astype(object)[None, None, :, None]).astype(np.uint64)
+            for p in range(parts)]
+    flat = list(np.concatenate(mids))
+    (got_row,) = read_partition(os.path.join(storage, "sd", "fo", "0"))
+    got = parse_row(o, got_row)
+    want = _reduce_tree_chunked(o, flat, rlk, mul, 2)
+    assert np.array_equal(got, want)

@@ -9,9 +9,13 @@ NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 D=$ROOT/herdsman_amd/var/$NAME
 rm -rf "$D"; mkdir -p "$D/csrc"
-cp "$ROOT"/herdsman_amd/csrc/* "$D/csrc/"
 if [ -n "$REV" ]; then
-  for f in "$D"/csrc/*; do git -C "$ROOT" show "$REV:herdsman_amd/csrc/$(basename "$f")" > "$f"; done
+  # the source list of that revision (files were added and split between rounds)
+  for f in $(git -C "$ROOT" ls-tree --name-only "$REV" herdsman_amd/csrc/); do
+    git -C "$ROOT" show "$REV:$f" > "$D/csrc/$(basename "$f")"
+  done
+else
+  cp "$ROOT"/herdsman_amd/csrc/* "$D/csrc/"
 fi
 sed -i "s@\"../../include/plugins/fhe_backend.h\"@\"plugins/fhe_backend.h\"@" "$D"/csrc/*.hpp "$D"/csrc/*.cpp "$D"/csrc/*.hip
 while [ $# -ge 2 ]; do sed -i "$1" "$D/csrc/$2"; shift 2; done
