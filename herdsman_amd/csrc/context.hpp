@@ -55,6 +55,7 @@ struct ConvTab {
 struct fhe_ctx {
   fhe_params params{};
   int device = 0;
+  u32 num_cus = 256;  // compute units of the device (persistent grids)
   hipStream_t stream = nullptr;
   hipStream_t own_stream = nullptr;  // fhe_use_own_stream
   std::string err;

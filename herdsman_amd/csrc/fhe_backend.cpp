@@ -426,6 +426,9 @@ int fhe_ctx_create(const fhe_params *params, int device, fhe_ctx **out) {
   fhe_ctx *c = new (std::nothrow) fhe_ctx();
   if (!c) return FHE_ERR_OOM;
   c->device = device;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    c->num_cus = (u32)ncu;
   int rc = ctx_build(c, params);
   if (rc) {
     g_create_error = c->err;

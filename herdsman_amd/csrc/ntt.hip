@@ -9,6 +9,26 @@ int ntt_col_plain(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) { return c
 int ntt_row_plain(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) { return row_pass(c, a, inv, n_jobs); }
 
 
+#ifndef NTT_PERSIST
+#define NTT_PERSIST 14  // plain NTTs at log_n in [NTT_PERSIST, 14] run the persistent one-pass kernel (15: none)
+#endif
+
+// the persistent one-residue-per-workgroup pass (ntt_persist), or 1 if the
+// launch's moduli mix both lazy-schedule classes (the two-pass path takes it)
+// Special moduli only: generic moduli keep the two-pass path, because ROCm
+// 7.2's backend fails some generic instantiations of the multi-residue kernel
+// ("illegal VGPR to SGPR copy": the inverse, the narrow forward schedule).
+template <int LOG_N>
+static int persist(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  if (!c->special) return 1;
+  if (inv) return launch_persist<LOG_N, true, true, 0>(c, a, n_jobs);
+  switch (wide_mode(c, a.map)) {
+    case 1: return launch_persist<LOG_N, false, true, 1>(c, a, n_jobs);
+    case 0: return launch_persist<LOG_N, false, true, 0>(c, a, n_jobs);
+  }
+  return 1;
+}
+
 int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool lazy_out, const u64 *scale,
                const u64 *src) {
   const u32 n_jobs = m.n_polys * m.cnt;
@@ -40,8 +60,13 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
   // N = 2^14: two passes of 7 stages with 32 sub-transforms per workgroup (35 KiB
   // of LDS, 4 workgroups per CU) instead of one pass per residue (128 KiB,
   // one workgroup of 16 waves per CU)
-  if (c->log_n <= 13) return single_pass(c, a, inverse, n_jobs);
   int rc;
+  if (c->log_n >= NTT_PERSIST && c->log_n <= 14) {
+    rc = c->log_n == 14 ? persist<14>(c, a, inverse, n_jobs)
+                        : NTT_PERSIST <= 13 ? persist<NTT_PERSIST <= 13 ? 13 : 14>(c, a, inverse, n_jobs) : 1;
+    if (rc != 1) return rc;
+  }
+  if (c->log_n <= 13) return single_pass(c, a, inverse, n_jobs);
   if (!inverse) {
     rc = col_pass(c, a, false, n_jobs);
     if (rc) return rc;

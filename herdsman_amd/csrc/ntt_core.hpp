@@ -31,6 +31,7 @@
 // data nor the twiddle latency sits on the VALU critical path.
 #pragma once
 #include <algorithm>
+#include <type_traits>
 
 #include "context.hpp"
 
@@ -242,6 +243,22 @@ __device__ __forceinline__ void st_e(u64 *base, u32 off, u64 v) {
   if constexpr (NTT_NTST & 2) __builtin_nontemporal_store(v, (u64 *)((char *)base + off));
   else st_b(base, off, v);
 }
+// 16-byte accesses of two adjacent words (PAIR_IO): an L2-served 16-B load per
+// lane moves 1.8x the bytes per second of an 8-B one (30-36 against 17-19 TB/s,
+// profiles/r05/microbench_stream_l2.txt)
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u64x2 ld2_b(const u64 *base, u32 off) { return *(const u64x2 *)((const char *)base + off); }
+__device__ __forceinline__ u64x2 ld2_d(const u64 *base, u32 off) {
+  return __builtin_nontemporal_load((const u64x2 *)((const char *)base + off));
+}
+__device__ __forceinline__ void st2_d(u64 *base, u32 off, u64x2 v) {
+  if constexpr (NTT_NTST & 1) __builtin_nontemporal_store(v, (u64x2 *)((char *)base + off));
+  else *(u64x2 *)((char *)base + off) = v;
+}
+__device__ __forceinline__ void st2_e(u64 *base, u32 off, u64x2 v) {
+  if constexpr (NTT_NTST & 2) __builtin_nontemporal_store(v, (u64x2 *)((char *)base + off));
+  else *(u64x2 *)((char *)base + off) = v;
+}
 
 #ifndef LDS_PAD
 #define LDS_PAD 1  // 0: unpadded exchange tile (32 KiB at S = 8, W = 16: 5 workgroups per CU, bank conflicts)
@@ -297,6 +314,27 @@ struct Grp {
   }
 };
 
+#ifndef PAIR_IO
+#define PAIR_IO 1  // 16-byte HBM/L2 accesses on the re-laid-out side of row passes (0: 8-byte, group-0 layout)
+#endif
+// The HBM-facing layout of the side of a row (or single) pass that goes
+// through an LDS re-layout anyway: the forward pass's store and its epilogue
+// operands, the inverse pass's load and its prologue operands.  With PAIR_IO,
+// thread ts of a T-thread sub-transform owns words 2ts and 2ts + 1 of every
+// 2T-word run, so each pair (registers 2j, 2j + 1) is one 16-byte access
+// and a wave instruction moves four 256 B segments; else the group-0
+// layout (words ts + T r, 8-byte accesses).  Thread and register bits are
+// disjoint either way, so the LDS pad splits between them (lds_pad).
+template <int S, int LOGR, bool P = PAIR_IO>
+struct IoL {
+  static constexpr u32 T = 1u << (S - LOGR);
+  static constexpr int STEP = P ? 2 : 1;  // words per access
+  __device__ static __forceinline__ u32 k_thr(u32 ts) { return P ? ts << 1 : Grp<S, LOGR, 0>::k_thr(ts); }
+  static constexpr u32 k_reg(int r) {
+    return P ? ((u32)(r & 1) | ((u32)(r >> 1) * 2 * T)) : Grp<S, LOGR, 0>::k_reg(r);
+  }
+};
+
 // x - m if that is non-negative, else x (x, m < 2^63; neg_m = -m), selected
 // by the sign word with two v_bfi_b32: no VCC compare/select, so no hazard nops
 __device__ __forceinline__ u64 harvey_csub(u64 x, u64 neg_m) {
@@ -318,7 +356,10 @@ __device__ __forceinline__ u64 harvey_csub(u64 x, u64 neg_m) {
 // below 8q < 2^63; the last stage canonicalises from [0,8q).
 __host__ __device__ constexpr bool wide_csub(int gs) { return gs >= 2 && (gs & 1) == 0; }
 
-template <int S, int LOGR, int G, int S0, bool INV, bool SP, bool WIDE>
+// LSW: butterflies per lock-step chunk (all R/2 of a stage by default; the
+// persistent single pass, which also holds the next residue, takes 4 so the
+// products' temporaries fit beside its second register tile)
+template <int S, int LOGR, int G, int S0, bool INV, bool SP, bool WIDE, int LSW = 8>
 __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 q2, const ModInfo &mi) {
   using GP = Grp<S, LOGR, G>;
   constexpr int R = 1 << LOGR;
@@ -327,10 +368,10 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
     const int tau = INV ? GP::nb - 1 - ti : ti;
     const int half = 1 << (GP::nb - 1 - tau);
     if constexpr (SP || GEN_VEC) {
-      // the R/2 butterflies of this stage in lock-step (see mont_mul_sp_vec)
-      constexpr int H = R / 2;
-      u64 A[H], Wt[H], V[H], U[H];
-      int lo_idx[H];
+      // the R/2 butterflies of this stage in lock-step (see mont_mul_sp_vec),
+      // CH at a time
+      constexpr int H = R / 2, CH = LSW < H ? LSW : H;
+      int lo_idx[H], w_idx[H];
       {
         int n = 0;
 #pragma unroll
@@ -338,7 +379,7 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
           const int rb = r & ((1 << GP::nb) - 1), rx = r >> GP::nb;
           if (rb & half) continue;
           lo_idx[n] = r;
-          Wt[n] = t[GP::slot(tau, rx, rb >> (GP::nb - tau))];
+          w_idx[n] = GP::slot(tau, rx, rb >> (GP::nb - tau));
           ++n;
         }
       }
@@ -351,26 +392,31 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
       const int gs = S0 + G * LOGR + tau;  // global stage
       const bool red = !WIDE || wide_csub(gs);
 #pragma unroll
-      for (int i = 0; i < H; ++i) {
-        const u64 X = x[lo_idx[i]], Y = x[lo_idx[i] + half];
-        if (!INV) {
-          U[i] = !red ? X : harvey_csub(X, WIDE ? nq4 : nq2);
-          A[i] = Y;
-        } else {
-          U[i] = harvey_csub(X + Y, nq2);
-          A[i] = (X + q2p1) + ~Y;
-        }
-      }
-      if constexpr (SP) mont_mul_sp_vec<H>(V, A, Wt, mi.q_hi);
-      else mont_mul_gen_vec<H>(V, A, Wt, mi);
+      for (int c0 = 0; c0 < H; c0 += CH) {
+        u64 A[CH], Wt[CH], V[CH], U[CH];
 #pragma unroll
-      for (int i = 0; i < H; ++i) {
-        if (!INV) {
-          x[lo_idx[i]] = U[i] + V[i];
-          x[lo_idx[i] + half] = (U[i] + q2p1) + ~V[i];
-        } else {
-          x[lo_idx[i]] = U[i];
-          x[lo_idx[i] + half] = V[i];
+        for (int i = 0; i < CH; ++i) {
+          const u64 X = x[lo_idx[c0 + i]], Y = x[lo_idx[c0 + i] + half];
+          Wt[i] = t[w_idx[c0 + i]];
+          if (!INV) {
+            U[i] = !red ? X : harvey_csub(X, WIDE ? nq4 : nq2);
+            A[i] = Y;
+          } else {
+            U[i] = harvey_csub(X + Y, nq2);
+            A[i] = (X + q2p1) + ~Y;
+          }
+        }
+        if constexpr (SP) mont_mul_sp_vec<CH>(V, A, Wt, mi.q_hi);
+        else mont_mul_gen_vec<CH>(V, A, Wt, mi);
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          if (!INV) {
+            x[lo_idx[c0 + i]] = U[i] + V[i];
+            x[lo_idx[c0 + i] + half] = (U[i] + q2p1) + ~V[i];
+          } else {
+            x[lo_idx[c0 + i]] = U[i];
+            x[lo_idx[c0 + i] + half] = V[i];
+          }
         }
       }
       continue;
@@ -414,10 +460,21 @@ struct PassGeo {
   static constexpr bool LAST = single || (COLS == INV);
 };
 
-template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, bool WIDE, int EPI, int GI>
+#ifndef PERSIST_LSW
+#define PERSIST_LSW 2  // lock-step butterflies per chunk in the persistent single pass (run_group LSW)
+#endif
+// group_loop's hook between a group's twiddle prefetch and its butterflies
+// (the persistent single pass loads the next residue there, ResidueFetch)
+struct NoFetch {
+  template <int GI, int NG>
+  __device__ __forceinline__ void issue() {}
+};
+
+template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, bool WIDE, int EPI, int GI,
+          class PF = NoFetch>
 __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds, const u64 *tw, u64 *data,
                                            u32 voff, u32 w, u32 ts, u32 hi, const NttArgs &a,
-                                           const ModInfo &mi, u32 mod, const EpiRow &ep) {
+                                           const ModInfo &mi, u32 mod, const EpiRow &ep, PF &pf) {
   using PG = PassGeo<LOG_N, S, COLS, INV>;
   constexpr int NG = (S + LOGR - 1) / LOGR;
   constexpr int R = 1 << LOGR;
@@ -426,9 +483,15 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
   const u64 q = mi.q, q2 = 2 * q;
   if constexpr (GI + 1 < NG) {
     constexpr int GN = INV ? NG - 2 - GI : GI + 1;
+    // the next group's twiddles are in flight while this group computes; with
+    // a residue fetch riding along (ntt_persist) they are loaded after it
+    // instead, under the exchange (the second register tile leaves no room)
+    constexpr bool TW_AHEAD = std::is_same<PF, NoFetch>::value;
     u64 tn[16];
-    Grp<S, LOGR, GN>::template load_tw<PG::S0>(tn, tw, hi, ts);  // in flight while this group computes
-    run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
+    if constexpr (TW_AHEAD) Grp<S, LOGR, GN>::template load_tw<PG::S0>(tn, tw, hi, ts);
+    pf.template issue<GI, NG>();
+    run_group<S, LOGR, G, PG::S0, INV, SP, WIDE, TW_AHEAD ? 8 : PERSIST_LSW>(x, tc, q2, mi);
+    if constexpr (!TW_AHEAD) Grp<S, LOGR, GN>::template load_tw<PG::S0>(tn, tw, hi, ts);
     const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + lds_pad(GP::k_reg(r))] = x[r];
@@ -440,24 +503,41 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
       x[r] = lds[lr + kr + lds_pad(kr)];
     }
     group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, GI + 1>(x, tn, lds, tw, data, voff, w, ts, hi, a, mi,
-                                                                     mod, ep);
+                                                                     mod, ep, pf);
   } else {
     // EPI_COMBINE: the epilogue's acc and base words are in flight while the
     // last group computes (the LDS footprint caps occupancy at 4 waves per
     // SIMD, so the 128-VGPR budget has room for them)
     constexpr int RE = is_combine(EPI) ? R : 1;
+    using IO = IoL<S, LOGR>;
     u64 pa[RE], pb[RE];
     if constexpr (is_combine(EPI)) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if constexpr (EPI == EPI_COMBINE) pa[r] = ld_b(ep.acc + Grp<S, LOGR, 0>::k_reg(r), voff);
-        const u32 kr = Grp<S, LOGR, 0>::k_reg(r);
-        if (!ep.add) pb[r] = 0;
-        else if (ep.g) pb[r] = ld_b(ep.base, aut_src<LOG_N>((voff >> 3) + kr, ep.g));  // sigma_g(base)
-        else pb[r] = ld_b(ep.base + kr, voff);
+      for (int r = 0; r < R; r += IO::STEP) {
+        const u32 kr = IO::k_reg(r);
+        if constexpr (IO::STEP == 2) {
+          if constexpr (EPI == EPI_COMBINE) {
+            const u64x2 v = ld2_b(ep.acc + kr, voff);
+            pa[r] = v.x, pa[r + 1] = v.y;
+          }
+          if (!ep.add) {
+            pb[r] = pb[r + 1] = 0;
+          } else if (ep.g) {  // sigma_g(base): a gather, word by word
+            pb[r] = ld_b(ep.base, aut_src<LOG_N>((voff >> 3) + kr, ep.g));
+            pb[r + 1] = ld_b(ep.base, aut_src<LOG_N>((voff >> 3) + kr + 1, ep.g));
+          } else {
+            const u64x2 v = ld2_b(ep.base + kr, voff);
+            pb[r] = v.x, pb[r + 1] = v.y;
+          }
+        } else {
+          if constexpr (EPI == EPI_COMBINE) pa[r] = ld_b(ep.acc + kr, voff);
+          if (!ep.add) pb[r] = 0;
+          else if (ep.g) pb[r] = ld_b(ep.base, aut_src<LOG_N>((voff >> 3) + kr, ep.g));  // sigma_g(base)
+          else pb[r] = ld_b(ep.base + kr, voff);
+        }
       }
     }
-    run_group<S, LOGR, G, PG::S0, INV, SP, WIDE>(x, tc, q2, mi);
+    run_group<S, LOGR, G, PG::S0, INV, SP, WIDE, std::is_same<PF, NoFetch>::value ? 8 : PERSIST_LSW>(x, tc, q2, mi);
     // negated reduction constants pinned in SGPRs, so each conditional
     // subtraction is one v_lshl_add_u64 with a scalar operand (left to itself
     // the compiler forms x - m as a v_subrev_co/v_subb_co borrow chain with
@@ -497,90 +577,111 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     }
     if constexpr (!COLS && G != 0) {
       // EPI_KSQ: the key-switching operands (ext and key words, KD of each per
-      // element) are software-pipelined PD elements deep, and the first PD
-      // elements' loads are in flight across the re-layout barrier
+      // element) are software-pipelined PD elements (PAIR_IO: PD / 2 pairs)
+      // deep, and the first ones' loads are in flight across the re-layout barrier
       constexpr int KD = is_ksq(EPI) ? ksq_digits(EPI) : 1;
       constexpr int PD = is_ksq(EPI) && SP ? KSQ_PD : 1;
-      u64 ek[PD + 1][2 * KD];
-      if constexpr (is_ksq(EPI)) {
+      constexpr int ST = IO::STEP, NST = R / ST, PDS = (PD + ST - 1) / ST;
+      u64 ek[PDS + 1][2 * KD][ST];
+      const auto fetch = [&](int st, u64 (&slot)[2 * KD][ST]) {
+        const u32 kr = IO::k_reg(st * ST);
 #pragma unroll
-        for (int r = 0; r < PD; ++r) {
-          const u32 kr = Grp<S, LOGR, 0>::k_reg(r);
-          const u32 eo = ksq_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kr, ep.xg) : voff;
+        for (int j = 0; j < KD; ++j) {
+          if constexpr (ksq_gather(EPI)) {
 #pragma unroll
-          for (int j = 0; j < KD; ++j) {
-            ek[r][j] = ld_b(ep.kext + (ksq_gather(EPI) ? 0 : kr) + j * ep.ext_j, eo);
-            ek[r][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
+            for (int h = 0; h < ST; ++h)
+              slot[j][h] = ld_b(ep.kext + j * ep.ext_j, aut_src<LOG_N>((voff >> 3) + kr + h, ep.xg));
+          } else if constexpr (ST == 2) {
+            const u64x2 e2 = ld2_b(ep.kext + kr + j * ep.ext_j, voff);
+            slot[j][0] = e2.x, slot[j][1] = e2.y;
+          } else {
+            slot[j][0] = ld_b(ep.kext + kr + j * ep.ext_j, voff);
+          }
+          if constexpr (ST == 2) {
+            const u64x2 k2 = ld2_b(ep.kksk + j * ep.ksk_j + kr, voff);
+            slot[KD + j][0] = k2.x, slot[KD + j][1] = k2.y;
+          } else {
+            slot[KD + j][0] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
           }
         }
+      };
+      if constexpr (is_ksq(EPI)) {
+#pragma unroll
+        for (int st = 0; st < PDS; ++st) fetch(st, ek[st]);
       }
       // row pass ending in a group whose lanes each own contiguous words:
-      // re-layout through LDS so the HBM store is coalesced (group-0 layout)
+      // re-layout through LDS so the HBM store is coalesced (the IO layout)
       const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
 #pragma unroll
       for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + lds_pad(GP::k_reg(r))] = x[r];
       __syncthreads();
-      using G0 = Grp<S, LOGR, 0>;
-      const u32 lr = lds_idx<S>(w, G0::k_thr(ts));
+      const u32 lr = lds_idx<S>(w, IO::k_thr(ts));
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const u32 kr = G0::k_reg(r);
-        const u64 v = lds[lr + kr + lds_pad(kr)];
-        if constexpr (is_combine(EPI)) {
-          // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM.
-          // acc - conv is formed as acc + Bq - v (v < Bq, B = 4 WIDE / 2): below
-          // 5q < 2^63 for q < 2^60 and 3q < 2^63 for q < 2^61, inside the
-          // Montgomery input bound, whose product below 1.5q (2q generic)
-          // is canonicalised by one conditional subtraction
-          u64 acc;
-          if constexpr (is_ksq(EPI)) {
-            // acc_Q = sum_j ext_j ksk_j R^-1 (ext carries R), at the store
-            // position: acc_Q never makes an HBM round trip.  Each product is
-            // below 1.5q (2q generic), so one subtraction of 4q (WIDE) leaves
-            // the lazy sum below 4q; otherwise it is made canonical.
-            if (r + PD < R) {
-              const u32 kn = G0::k_reg(r + PD);
-              const u32 eo = ksq_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kn, ep.xg) : voff;
+      for (int st = 0; st < NST; ++st) {
+        if constexpr (is_ksq(EPI)) {
+          if (st + PDS < NST) fetch(st + PDS, ek[(st + PDS) % (PDS + 1)]);
+        }
+        u64 o[ST];
+#pragma unroll
+        for (int h = 0; h < ST; ++h) {
+          const int r = st * ST + h;
+          const u32 kr = IO::k_reg(r);
+          const u64 v = lds[lr + kr + lds_pad(kr)];
+          if constexpr (is_combine(EPI)) {
+            // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM.
+            // acc - conv is formed as acc + Bq - v (v < Bq, B = 4 WIDE / 2): below
+            // 5q < 2^63 for q < 2^60 and 3q < 2^63 for q < 2^61, inside the
+            // Montgomery input bound, whose product below 1.5q (2q generic)
+            // is canonicalised by one conditional subtraction
+            u64 acc;
+            if constexpr (is_ksq(EPI)) {
+              // acc_Q = sum_j ext_j ksk_j R^-1 (ext carries R), at the store
+              // position: acc_Q never makes an HBM round trip.  Each product is
+              // below 1.5q (2q generic), so one subtraction of 4q (WIDE) leaves
+              // the lazy sum below 4q; otherwise it is made canonical.
+              u64 e[KD], k[KD], pr[KD];
 #pragma unroll
               for (int j = 0; j < KD; ++j) {
-                ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + (ksq_gather(EPI) ? 0 : kn) + j * ep.ext_j, eo);
-                ek[(r + PD) % (PD + 1)][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
+                e[j] = ek[st % (PDS + 1)][j][h];
+                k[j] = ek[st % (PDS + 1)][KD + j][h];
               }
-            }
-            u64 e[KD], k[KD], pr[KD];
+              if constexpr (SP) {
+                mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+              } else if constexpr (GEN_VEC) {
+                mont_mul_gen_vec<KD>(pr, e, k, mi);
+              } else {
 #pragma unroll
-            for (int j = 0; j < KD; ++j) {
-              e[j] = ek[r % (PD + 1)][j];
-              k[j] = ek[r % (PD + 1)][KD + j];
-            }
-            if constexpr (SP) {
-              mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
-            } else if constexpr (GEN_VEC) {
-              mont_mul_gen_vec<KD>(pr, e, k, mi);
+                for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
+              }
+              acc = pr[0];
+              if constexpr (WIDE) {
+                // q < 2^60: the whole sum stays below 6q < 2^63
+#pragma unroll
+                for (int j = 1; j < KD; ++j) acc += pr[j];
+                if constexpr (KD > 2) acc = harvey_csub(acc, nq4);
+              } else {
+                // q < 2^61: keep the running sum below 2q, then canonical
+#pragma unroll
+                for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
+                acc = harvey_csub(acc, nq1);
+              }
             } else {
-#pragma unroll
-              for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
+              acc = pa[r];
             }
-            acc = pr[0];
-            if constexpr (WIDE) {
-              // q < 2^60: the whole sum stays below 6q < 2^63
-#pragma unroll
-              for (int j = 1; j < KD; ++j) acc += pr[j];
-              if constexpr (KD > 2) acc = harvey_csub(acc, nq4);
-            } else {
-              // q < 2^61: keep the running sum below 2q, then canonical
-#pragma unroll
-              for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
-              acc = harvey_csub(acc, nq1);
-            }
+            u64 ks = harvey_csub(mont_mul<SP>((acc + cb1) + ~v, ep.pinv, mi), nq1);
+            if (ep.add) ks = add_mod(ks, pb[r], q);
+            o[h] = ks;
           } else {
-            acc = pa[r];
+            o[h] = v;
           }
-          u64 ks = harvey_csub(mont_mul<SP>((acc + cb1) + ~v, ep.pinv, mi), nq1);
-          if (ep.add) ks = add_mod(ks, pb[r], q);
-          st_e(ep.out + kr, voff, ks);
+        }
+        const u32 ko = IO::k_reg(st * ST);
+        if constexpr (ST == 2) {
+          if constexpr (is_combine(EPI)) st2_e(ep.out + ko, voff, u64x2{o[0], o[1]});
+          else st2_d(data + ko, voff, u64x2{o[0], o[1]});
         } else {
-          st_d(data + kr, voff, v);
+          if constexpr (is_combine(EPI)) st_e(ep.out + ko, voff, o[0]);
+          else st_d(data + ko, voff, o[0]);
         }
       }
     } else {
@@ -602,63 +703,103 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
   constexpr int NG = (S + LOGR - 1) / LOGR;
   constexpr int G0 = INV ? NG - 1 : 0;
   u64 tc[16];
-  Grp<S, LOGR, G0>::template load_tw<PG::S0>(tc, tw, hi, ts);
+  // the first group's twiddles: a row pass with an operand prologue loads them
+  // after it (they are not needed before the re-layout, and held through the
+  // prologue they pushed the operand ring into spills)
+  constexpr bool TW_LATE = !COLS && G0 != 0 && EPI != EPI_NONE;
+  if constexpr (!TW_LATE) Grp<S, LOGR, G0>::template load_tw<PG::S0>(tc, tw, hi, ts);
   u64 x[R];
   u32 voff;  // byte offset of this thread's element k_thr of the first (HBM) group layout
   if constexpr (!COLS && G0 != 0) {
     // row pass starting in a per-lane-contiguous group: coalesced load in the
-    // group-0 layout, then one LDS re-layout
-    using GZ = Grp<S, LOGR, 0>;
+    // IO layout (16-byte pairs with PAIR_IO), then one LDS re-layout.  The
+    // key-switch prologue keeps 8-byte loads: with pairs of its 2 KD operand
+    // streams the compiler holds 12 KD words across steps and spills (61-139
+    // VGPRs at KD = 3-4 under the 4-wave bound)
+    using GZ = IoL<S, LOGR, PAIR_IO && !is_ksp(EPI)>;
+    constexpr int ST = GZ::STEP;
     voff = (gb + GZ::k_thr(ts)) << 3;
     if constexpr (EPI == PRO_TENSOR) {
       // the CKKS tensor formulas, element-wise at the coalesced positions.
-      // Software-pipelined PD elements deep: the operand loads of element
-      // r + PD are issued before element r's stores (the outputs may alias the
+      // Software-pipelined PD steps deep: the operand loads of step s + PD
+      // are issued before step s's stores (the outputs may alias the
       // operands element-wise only, so the compiler would otherwise wait for
-      // each element's loads right after the previous element's stores)
-      constexpr int PD = SP ? 2 : 0;  // the generic products need the registers
-      u64 op[PD + 1][4];
+      // each step's loads right after the previous step's stores)
+      constexpr int PD = SP ? (ST == 2 ? 1 : 2) : 0;  // the generic products need the registers
+      constexpr int NST = R / ST;
+      u64 op[PD + 1][4][ST];
+      const auto fetch = [&](int st, u64 (&o)[4][ST]) {
+        const u32 kn = GZ::k_reg(st * ST);
+        const u64 *src[4] = {ep.a0, ep.a1, ep.b0, ep.b1};
 #pragma unroll
-      for (int r = 0; r < PD; ++r) {
-        const u32 kr = GZ::k_reg(r);
-        op[r][0] = ld_b(ep.a0 + kr, voff), op[r][1] = ld_b(ep.a1 + kr, voff);
-        op[r][2] = ld_b(ep.b0 + kr, voff), op[r][3] = ld_b(ep.b1 + kr, voff);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const u32 kr = GZ::k_reg(r);
-        if (r + PD < R) {
-          const u32 kn = GZ::k_reg(r + PD);
-          u64(&o)[4] = op[(r + PD) % (PD + 1)];
-          o[0] = ld_b(ep.a0 + kn, voff), o[1] = ld_b(ep.a1 + kn, voff);
-          o[2] = ld_b(ep.b0 + kn, voff), o[3] = ld_b(ep.b1 + kn, voff);
+        for (int i = 0; i < 4; ++i) {
+          if constexpr (ST == 2) {
+            const u64x2 v = ld2_b(src[i] + kn, voff);
+            o[i][0] = v.x, o[i][1] = v.y;
+          } else {
+            o[i][0] = ld_b(src[i] + kn, voff);
+          }
         }
-        const u64 a0 = op[r % (PD + 1)][0], a1 = op[r % (PD + 1)][1];
-        const u64 b0 = op[r % (PD + 1)][2], b1 = op[r % (PD + 1)][3];
-        st_e(ep.o0 + kr, voff, mul_mod<SP>(a0, b0, mi));
-        U128 s = mul128(a0, b1);
-        mac128(s, a1, b0);
-        st_e(ep.o1 + kr, voff, reduce128<SP>(s, mi));
-        const u64 t = mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi);  // d2 in [0, 2q)
-        x[r] = csub(t, mi.q);
-        st_e(ep.ext + kr, voff, csub(mont_mul<SP>(t, mi.r2, mi), mi.q));  // d2 R
+      };
+#pragma unroll
+      for (int st = 0; st < PD; ++st) fetch(st, op[st]);
+#pragma unroll
+      for (int st = 0; st < NST; ++st) {
+        if (st + PD < NST) fetch(st + PD, op[(st + PD) % (PD + 1)]);
+        u64 o0[ST], o1[ST], oe[ST];
+#pragma unroll
+        for (int h = 0; h < ST; ++h) {
+          const u64 a0 = op[st % (PD + 1)][0][h], a1 = op[st % (PD + 1)][1][h];
+          const u64 b0 = op[st % (PD + 1)][2][h], b1 = op[st % (PD + 1)][3][h];
+          o0[h] = mul_mod<SP>(a0, b0, mi);
+          U128 sm = mul128(a0, b1);
+          mac128(sm, a1, b0);
+          o1[h] = reduce128<SP>(sm, mi);
+          const u64 t = mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi);  // d2 in [0, 2q)
+          x[st * ST + h] = csub(t, mi.q);
+          oe[h] = csub(mont_mul<SP>(t, mi.r2, mi), mi.q);  // d2 R
+        }
+        const u32 kr = GZ::k_reg(st * ST);
+        if constexpr (ST == 2) {
+          st2_e(ep.o0 + kr, voff, u64x2{o0[0], o0[1]});
+          st2_e(ep.o1 + kr, voff, u64x2{o1[0], o1[1]});
+          st2_e(ep.ext + kr, voff, u64x2{oe[0], oe[1]});
+        } else {
+          st_e(ep.o0 + kr, voff, o0[0]);
+          st_e(ep.o1 + kr, voff, o1[0]);
+          st_e(ep.ext + kr, voff, oe[0]);
+        }
       }
     } else if constexpr (EPI == PRO_BFVT) {
       // the BFV tensor formulas at the coalesced positions; e is per workgroup
+      const auto ld = [&](const u64 *base, int r0, u64 (&v)[ST]) {
+        if constexpr (ST == 2) {
+          const u64x2 t = ld2_b(base + GZ::k_reg(r0), voff);
+          v[0] = t.x, v[1] = t.y;
+        } else {
+          v[0] = ld_b(base + GZ::k_reg(r0), voff);
+        }
+      };
       if (ep.e == 1) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const u32 kr = GZ::k_reg(r);
-          U128 s = mul128(ld_b(ep.a0 + kr, voff), ld_b(ep.b1 + kr, voff));
-          mac128(s, ld_b(ep.a1 + kr, voff), ld_b(ep.b0 + kr, voff));
-          x[r] = reduce128<SP>(s, mi);
+        for (int r = 0; r < R; r += ST) {
+          u64 a0[ST], a1[ST], b0[ST], b1[ST];
+          ld(ep.a0, r, a0), ld(ep.b1, r, b1), ld(ep.a1, r, a1), ld(ep.b0, r, b0);
+#pragma unroll
+          for (int h = 0; h < ST; ++h) {
+            U128 sm = mul128(a0[h], b1[h]);
+            mac128(sm, a1[h], b0[h]);
+            x[r + h] = reduce128<SP>(sm, mi);
+          }
         }
       } else {
         // e = 0: (a0, b0), e = 2: (a1, b1) -- the pair is resolved in ntt_pass
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const u32 kr = GZ::k_reg(r);
-          x[r] = mul_mod<SP>(ld_b(ep.a0 + kr, voff), ld_b(ep.b0 + kr, voff), mi);
+        for (int r = 0; r < R; r += ST) {
+          u64 a0[ST], b0[ST];
+          ld(ep.a0, r, a0), ld(ep.b0, r, b0);
+#pragma unroll
+          for (int h = 0; h < ST; ++h) x[r + h] = mul_mod<SP>(a0[h], b0[h], mi);
         }
       }
     } else if constexpr (EPI == PRO_AUTOMORPH) {
@@ -689,57 +830,75 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       // acc_P = sum_j ext_j ksk_j R^-1 (ks_inner_kernel; ext carries R) at the
       // coalesced positions, canonical: the products are below 1.5q (2q
       // generic), the running sum is kept below 2q.  Operands software-
-      // pipelined PD elements deep (as EPI_KSQ)
+      // pipelined PD elements (PD / 2 pairs) deep (as EPI_KSQ)
       constexpr int KD = ksp_digits(EPI);
       constexpr int PD = SP || ksp_gather(EPI) ? KSP_PD : 1;
+      constexpr int NST = R / ST, PDS = (PD + ST - 1) / ST;
       u64 nq1 = 0 - mi.q, nq2 = 0 - 2 * mi.q;
       asm("" : "+s"(nq1));
       asm("" : "+s"(nq2));
-      u64 ek[PD + 1][2 * KD];
-#pragma unroll
-      for (int r = 0; r < PD; ++r) {
-        const u32 kr = GZ::k_reg(r);
-        const u32 eo = ksp_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kr, ep.xg) : voff;
+      u64 ek[PDS + 1][2 * KD][ST];
+      const auto fetch = [&](int st, u64 (&slot)[2 * KD][ST]) {
+        const u32 kn = GZ::k_reg(st * ST);
 #pragma unroll
         for (int j = 0; j < KD; ++j) {
-          ek[r][j] = ld_b(ep.kext + (ksp_gather(EPI) ? 0 : kr) + j * ep.ext_j, eo);
-          ek[r][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kr, voff);
-        }
-      }
+          if constexpr (ksp_gather(EPI)) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (r + PD < R) {
-          const u32 kn = GZ::k_reg(r + PD);
-          const u32 eo = ksp_gather(EPI) ? aut_src<LOG_N>((voff >> 3) + kn, ep.xg) : voff;
-#pragma unroll
-          for (int j = 0; j < KD; ++j) {
-            ek[(r + PD) % (PD + 1)][j] = ld_b(ep.kext + (ksp_gather(EPI) ? 0 : kn) + j * ep.ext_j, eo);
-            ek[(r + PD) % (PD + 1)][KD + j] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
+            for (int h = 0; h < ST; ++h)
+              slot[j][h] = ld_b(ep.kext + j * ep.ext_j, aut_src<LOG_N>((voff >> 3) + kn + h, ep.xg));
+          } else if constexpr (ST == 2) {
+            const u64x2 e2 = ld2_b(ep.kext + kn + j * ep.ext_j, voff);
+            slot[j][0] = e2.x, slot[j][1] = e2.y;
+          } else {
+            slot[j][0] = ld_b(ep.kext + kn + j * ep.ext_j, voff);
+          }
+          if constexpr (ST == 2) {
+            const u64x2 k2 = ld2_b(ep.kksk + j * ep.ksk_j + kn, voff);
+            slot[KD + j][0] = k2.x, slot[KD + j][1] = k2.y;
+          } else {
+            slot[KD + j][0] = ld_b(ep.kksk + j * ep.ksk_j + kn, voff);
           }
         }
-        u64 e[KD], k[KD], pr[KD];
+      };
 #pragma unroll
-        for (int j = 0; j < KD; ++j) {
-          e[j] = ek[r % (PD + 1)][j];
-          k[j] = ek[r % (PD + 1)][KD + j];
+      for (int st = 0; st < PDS; ++st) fetch(st, ek[st]);
+#pragma unroll
+      for (int st = 0; st < NST; ++st) {
+        if (st + PDS < NST) fetch(st + PDS, ek[(st + PDS) % (PDS + 1)]);
+#pragma unroll
+        for (int h = 0; h < ST; ++h) {
+          u64 e[KD], k[KD], pr[KD];
+#pragma unroll
+          for (int j = 0; j < KD; ++j) {
+            e[j] = ek[st % (PDS + 1)][j][h];
+            k[j] = ek[st % (PDS + 1)][KD + j][h];
+          }
+          if constexpr (SP) {
+            mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+          } else if constexpr (GEN_VEC) {
+            mont_mul_gen_vec<KD>(pr, e, k, mi);
+          } else {
+#pragma unroll
+            for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
+          }
+          u64 acc = pr[0];
+#pragma unroll
+          for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
+          x[st * ST + h] = harvey_csub(acc, nq1);
         }
-        if constexpr (SP) {
-          mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
-        } else if constexpr (GEN_VEC) {
-          mont_mul_gen_vec<KD>(pr, e, k, mi);
-        } else {
-#pragma unroll
-          for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
-        }
-        u64 acc = pr[0];
-#pragma unroll
-        for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
-        x[r] = harvey_csub(acc, nq1);
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) x[r] = ld_d(data + GZ::k_reg(r), voff);
+      for (int r = 0; r < R; r += ST) {
+        if constexpr (ST == 2) {
+          const u64x2 v = ld2_d(data + GZ::k_reg(r), voff);
+          x[r] = v.x, x[r + 1] = v.y;
+        } else {
+          x[r] = ld_d(data + GZ::k_reg(r), voff);
+        }
+      }
     }
+    if constexpr (TW_LATE) Grp<S, LOGR, G0>::template load_tw<PG::S0>(tc, tw, hi, ts);
     const u32 lw = lds_idx<S>(w, GZ::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) lds[lw + GZ::k_reg(r) + lds_pad(GZ::k_reg(r))] = x[r];
@@ -801,10 +960,134 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
     constexpr int GL = INV ? 0 : NG - 1;
     voff = (gb + (Grp<S, LOGR, GL>::k_thr(ts) << PG::LS)) << 3;
   } else {
-    voff = (gb + Grp<S, LOGR, 0>::k_thr(ts)) << 3;
+    // forward: the re-laid-out IO layout (group_loop's store); inverse: the
+    // last group is group 0 and stores straight from registers
+    voff = (gb + (INV ? Grp<S, LOGR, 0>::k_thr(ts) : IoL<S, LOGR>::k_thr(ts))) << 3;
   }
-  group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, 0>(x, tc, lds, tw, data, voff, w, ts, hi, a, mi, mod, ep);
+  NoFetch nf;
+  group_loop<LOG_N, S, LOGR, W, INV, COLS, SP, WIDE, EPI, 0>(x, tc, lds, tw, data, voff, w, ts, hi, a, mi, mod, ep,
+                                                             nf);
 }
+
+// ---- persistent one-residue-per-workgroup pass (N = 2^13, 2^14; plain NTT/INTT)
+// A one-shot single pass at N = 2^14 holds a 128 KiB residue in one 1024-thread
+// workgroup per CU, so its HBM loads, butterflies, barrier-separated exchanges
+// and stores run one after the other with nothing to overlap them (it lost to
+// two 7-stage passes).  Here each workgroup loops over residues and loads the
+// NEXT residue's 16 words per thread into a second register tile while the
+// current one is transformed: the loads are issued in pieces behind each
+// group's twiddle prefetch (vmcnt counts in issue order, so a piece issued
+// there does not delay the waits of the group it rides on), and the stores of
+// residue j drain under the transform of residue j + 1.
+#ifndef PERSIST_FETCH
+#define PERSIST_FETCH 8  // words of the next residue prefetched per thread (the rest load when it starts)
+#endif
+template <class LAYOUT>
+struct ResidueFetch {
+  u64 (&nx)[16];
+  const u64 *src;  // the next residue (null: none)
+  u32 voff;        // this thread's element of the load layout
+  // piece GI of NG - 1: the PERSIST_FETCH loads spread over the groups that load twiddles
+  template <int GI, int NG>
+  __device__ __forceinline__ void issue() {
+    constexpr int F = PERSIST_FETCH, P = NG - 1, lo = F * GI / P, hi = F * (GI + 1) / P;
+    if (!src) return;
+#pragma unroll
+    for (int r = lo; r < hi; ++r) nx[r] = ld_d(src + LAYOUT::k_reg(r), voff);
+  }
+};
+
+
+template <int LOG_N, bool INV, bool SP, int WM, int K>
+__global__ void __launch_bounds__(1 << (LOG_N - 4)) ntt_persist(NttArgs a, u32 n_jobs) {
+  constexpr int S = LOG_N, LOGR = 4, W = 1, R = 16;
+  constexpr bool WIDE = !INV && WM == 1;
+  static_assert(WM != 2 || INV, "one lazy schedule class per persistent launch");
+  using PG = PassGeo<LOG_N, S, false, INV>;
+  static_assert(PG::single && PG::LAST, "one pass per residue");
+  constexpr int NG = (S + LOGR - 1) / LOGR;
+  constexpr int G0 = INV ? NG - 1 : 0;
+  // loads: forward in the first group's own (group-0) layout, inverse in the
+  // IO layout followed by an LDS re-layout; stores: forward through the
+  // re-layout into the IO layout, inverse straight from group 0
+  using GZ = typename std::conditional<INV, IoL<S, LOGR>, Grp<S, LOGR, 0>>::type;
+  using GS = typename std::conditional<INV, Grp<S, LOGR, 0>, IoL<S, LOGR>>::type;
+  using GF = Grp<S, LOGR, G0>;
+  extern __shared__ u64 lds[];
+  const u32 ts = threadIdx.x, w = 0, hi = 0;
+  const u32 voff = GZ::k_thr(ts) << 3, voff_st = GS::k_thr(ts) << 3;
+  const u32 np = a.map.n_polys;
+  // residue j of this workgroup: job blockIdx.x + j gridDim.x (K residues per
+  // workgroup, the loop fully unrolled: no loop-carried modulus or address)
+  const auto residue = [&](int j, u32 &mod) -> u64 * {
+    const u32 job = blockIdx.x + (u32)j * gridDim.x;
+    if (job >= n_jobs) return nullptr;
+    const u32 poly = job % np, limb = limbmap_limb(a.map, job / np);
+    mod = __builtin_amdgcn_readfirstlane(a.map.mod_offset + limb);
+    const size_t off = ((size_t)poly * a.map.poly_stride + limb) << LOG_N;
+    // uniform: SGPRs (readfirstlane) -- without it the compiler left the second
+    // residue's offset in VGPRs and failed ("illegal VGPR to SGPR copy")
+    const u32 lo = __builtin_amdgcn_readfirstlane((u32)off), hi32 = __builtin_amdgcn_readfirstlane((u32)(off >> 32));
+    return a.map.base + (((size_t)hi32 << 32) | lo);
+  };
+  const auto source = [&](u64 *d) -> const u64 * {  // the first forward pass may read out of place
+    return d && !INV && a.src ? a.src + (d - a.map.base) : d;
+  };
+  u64 x[R], nx[R];
+  u32 mod = 0;
+  u64 *data = residue(0, mod);
+  if (!data) return;
+  {
+    const u64 *din = source(data);
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = ld_d(din + GZ::k_reg(r), voff);
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    u32 nmod = 0;
+    u64 *ndata = j + 1 < K ? residue(j + 1, nmod) : nullptr;
+    ResidueFetch<GZ> pf{nx, source(ndata), voff};
+    const ModInfo mi = a.mods[mod];
+    const u64 *tw = a.tw + ((size_t)mod << LOG_N);
+    u64 tc[16];
+    GF::template load_tw<PG::S0>(tc, tw, hi, ts);
+    if constexpr (G0 != 0) {
+      // inverse: from the coalesced layout into the first (per-lane-contiguous) group's
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds[lds_idx<S>(w, GZ::k_thr(ts)) + GZ::k_reg(r) + lds_pad(GZ::k_reg(r))] = x[r];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32 kr = GF::k_reg(r);
+        x[r] = lds[lds_idx<S>(w, GF::k_thr(ts)) + kr + lds_pad(kr)];
+      }
+    }
+    EpiRow ep{};
+    group_loop<LOG_N, S, LOGR, W, INV, false, SP, WIDE, EPI_NONE, 0>(x, tc, lds, tw, data, voff_st, w, ts, hi, a,
+                                                                     mi, mod, ep, pf);
+    if (!ndata) return;
+    __syncthreads();  // this residue's last LDS reads before the next one's first writes
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = r < PERSIST_FETCH ? nx[r] : ld_d(pf.src + GZ::k_reg(r), voff);
+    mod = nmod;
+    data = ndata;
+  }
+}
+
+#ifndef PERSIST_K
+#define PERSIST_K 4  // residues per workgroup of the one-pass kernel (its register double buffer runs across them)
+#endif
+// one-pass launch: ceil(n_jobs / K) workgroups of K residues each
+template <int LOG_N, bool INV, bool SP, int WM>
+int launch_persist(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
+  constexpr size_t lds = lds_bytes<LOG_N, 1>();
+  auto k = ntt_persist<LOG_N, INV, SP, WM, PERSIST_K>;
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const u32 grid = (n_jobs + PERSIST_K - 1) / PERSIST_K;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(1u << (LOG_N - 4)), lds, c->stream, a, n_jobs);
+  return fhe_check(c, hipGetLastError(), "ntt_persist launch");
+}
+
 
 #ifndef NTT_MINW
 #define NTT_MINW 1
@@ -814,9 +1097,13 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 // workgroup branch between both; the kernel then carries both code paths and
 // needs ~150 VGPRs instead of ~90, i.e. 3 waves per SIMD instead of the 4 the
 // LDS allows: a launch over one modulus class avoids it)
+// The tensor prologue asks for 4 waves per SIMD (the LDS allows 4 workgroups
+// per CU anyway), so its 16-byte operand pairs stay within 128 VGPRs
+__host__ __device__ constexpr int pass_min_waves(int EPI, bool SP, int threads) {
+  return threads != 256 ? 1 : (PAIR_IO && EPI == PRO_TENSOR && SP) ? 4 : NTT_MINW;
+}
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int WM>
-__global__ void __launch_bounds__(W << (S - LOGR),
-                                  (W << (S - LOGR)) == 256 ? NTT_MINW : 1)
+__global__ void __launch_bounds__(W << (S - LOGR), pass_min_waves(EPI, SP, W << (S - LOGR)))
     ntt_pass(NttArgs a) {
   static_assert(is_combine(EPI) || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
                     EPI == PRO_BFVT || is_conv(EPI) || is_ksp(EPI),

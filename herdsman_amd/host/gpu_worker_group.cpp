@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <tuple>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -527,7 +528,7 @@ struct GpuWorkerGroup::Frames {
   std::deque<std::shared_ptr<ResidentFrame>> queue;              // waiting for the flusher
   std::map<std::string, std::shared_ptr<ResidentFrame>> pending;  // queued or being written
   bool stop = false, failed = false;
-  std::map<std::pair<int, int>, fhe_ctx *> flush_ctx;  // (device, schema) -> the flusher's context
+  std::map<std::tuple<uint32_t, int, int>, fhe_ctx *> flush_ctx;  // (flusher, device, schema) -> its context
   StageStats st;                                      // flushed rows and time
 
   // charge `need` bytes to the device, evicting least recently used frames
@@ -626,7 +627,9 @@ GpuWorkerGroup::GpuWorkerGroup(GpuWorkerGroupConfig config) : config_(std::move(
   for (auto &d : devices_)
     for (auto &l : d->lanes) l->thread = std::thread([this, dp = d.get(), lp = l.get()] { lane_loop(*dp, *lp); });
   completion_thread_ = std::thread([this] { completion_loop(); });
-  if (config_.write_behind) flush_thread_ = std::thread([this] { flush_loop(); });
+  if (config_.write_behind)
+    for (uint32_t i = 0; i < std::max(1u, config_.flush_threads); ++i)
+      flush_threads_.emplace_back([this, i] { flush_loop(i); });
 }
 
 GpuWorkerGroup::~GpuWorkerGroup() {
@@ -640,14 +643,14 @@ GpuWorkerGroup::~GpuWorkerGroup() {
   for (auto &d : devices_)
     for (auto &l : d->lanes) l->thread.join();
   // files written behind are committed before the group goes
-  if (flush_thread_.joinable()) {
+  if (!flush_threads_.empty()) {
     flush_frames();
     {
       std::lock_guard lk(frames_->m);
       frames_->stop = true;
     }
     frames_->cv.notify_all();
-    flush_thread_.join();
+    for (auto &t : flush_threads_) t.join();
   }
   // teardown order: resident frames, keys and lane buffers are freed through
   // their contexts, so they go before the contexts
@@ -1179,7 +1182,7 @@ bool GpuWorkerGroup::circuits_lowerable() noexcept { return lowerable_v<herd::co
 // write-behind: the flusher copies each queued resident frame back in chunks
 // (two pinned buffers, the next chunk's D2H under the current chunk's file
 // writes) on a context and stream of its own, and commits the partition file
-void GpuWorkerGroup::flush_loop() {
+void GpuWorkerGroup::flush_loop(uint32_t id) {
   constexpr size_t kRows = 16;
   Pinned stage[2];
   for (;;) {
@@ -1194,7 +1197,11 @@ void GpuWorkerGroup::flush_loop() {
     const auto t0 = std::chrono::steady_clock::now();
     std::string err;
     try {
-      fhe_ctx *&c = frames_->flush_ctx[std::make_pair(f->device, f->schema)];  // only this thread touches the map's values
+      fhe_ctx *c = nullptr;
+      {
+        std::lock_guard lk(frames_->m);
+        c = frames_->flush_ctx[std::make_tuple(id, f->device, f->schema)];
+      }
       if (!c) {
         const SchemaParams *sp = nullptr;
         for (const auto &x : config_.schemas)
@@ -1204,6 +1211,10 @@ void GpuWorkerGroup::flush_loop() {
         p.moduli = sp->moduli.empty() ? nullptr : sp->moduli.data();
         if (fhe_ctx_create(&p, f->device, &c) != FHE_OK)
           throw std::runtime_error(std::string("flusher fhe_ctx_create: ") + fhe_last_error(nullptr));
+        {
+          std::lock_guard lk(frames_->m);
+          frames_->flush_ctx[std::make_tuple(id, f->device, f->schema)] = c;
+        }
         ck(c, fhe_use_own_stream(c), "flusher stream");
       }
       PartitionWriter out(f->file, f->durable);

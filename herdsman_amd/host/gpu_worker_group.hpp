@@ -111,6 +111,7 @@ struct GpuWorkerGroupConfig {
   // file is committed; a task that must read a file still being flushed waits
   // for it.  Off by default: then a task completes after its file is committed.
   bool write_behind = false;
+  uint32_t flush_threads = 4;  // write-behind flusher threads (frames written in parallel)
 };
 
 class GpuWorkerGroup : public IWorkerGroup {
@@ -140,7 +141,7 @@ class GpuWorkerGroup : public IWorkerGroup {
 
   void lane_loop(Device &dev, Lane &lane);
   void completion_loop();
-  void flush_loop();
+  void flush_loop(uint32_t id);
   void complete(const std::shared_ptr<Handle> &h, TaskHandle::Status st);
 
   GpuWorkerGroupConfig config_;
@@ -155,7 +156,7 @@ class GpuWorkerGroup : public IWorkerGroup {
   std::mutex stats_m_;
   StageStats stats_;
   std::unique_ptr<Frames> frames_;  // resident frames and the write-behind flusher
-  std::thread flush_thread_;
+  std::vector<std::thread> flush_threads_;
 };
 
 class GpuWorkerGroup::Handle : public IWorkerGroup::TaskHandle {

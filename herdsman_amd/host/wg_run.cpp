@@ -135,6 +135,7 @@ static void env_config(GpuWorkerGroupConfig &cfg) {
   if (const char *t = std::getenv("WG_IO_THREADS")) cfg.io_threads = (uint32_t)std::max(1, std::atoi(t));
   if (const char *v = std::getenv("WG_RESIDENT_BYTES")) cfg.resident_frame_bytes = std::strtoull(v, nullptr, 10);
   if (const char *v = std::getenv("WG_WRITE_BEHIND")) cfg.write_behind = v[0] == '1';
+  if (const char *v = std::getenv("WG_FLUSH_THREADS")) cfg.flush_threads = (uint32_t)std::atoi(v);
 }
 
 // Keep concurrent_workers() tasks in flight, as the Executor does
@@ -273,7 +274,7 @@ static int bench(int argc, char **argv) {
   const bool chain = mode == "chainbench";
   std::vector<double> rates, rates2, rates2f;
   GpuWorkerGroup g(cfg);  // one long-lived group, as in a server
-  herdsman_gpu::StageStats st1;
+  herdsman_gpu::StageStats st1, st2;
   for (int rep = 0; rep <= reps; ++rep) {  // rep 0 warms contexts, keys, pinned and device buffers
     // each repetition writes fresh output frames, as every herdsman job does
     const std::string mid = "out" + std::to_string(rep), fin = "fin" + std::to_string(rep);
@@ -281,20 +282,20 @@ static int bench(int argc, char **argv) {
       std::filesystem::remove_all(cfg.storage_dir / "bench" / ("out" + std::to_string(rep - 1)));
       std::filesystem::remove_all(cfg.storage_dir / "bench" / ("fin" + std::to_string(rep - 1)));
     }
-    if (rep == 1) g.reset_stage_stats();
+    g.reset_stage_stats();
     // stage 1: "in0 in1 mul" over the input partitions (files)
     const double dt = run_all(g, parts, [&](int p) { return task("in", mid, p, mul2); });
     const double rate = (double)parts * rows / dt;
     std::printf("%s rep %d: %d MapTasks x %d rows in %.3f s = %.1f ct-mult+relin/s (%zu workers)\n",
                 chain ? "stage-1" : "bench", rep, parts, rows, dt, rate, g.concurrent_workers());
     if (rep) rates.push_back(rate);
-    if (!chain) continue;
-    if (!g.flush_frames()) throw std::runtime_error("write-behind failed");  // stage 1's files, off the clock
-    if (rep) {
-      herdsman_gpu::StageStats a = g.stage_stats();
-      st1 += a;
-      g.reset_stage_stats();
+    if (!chain) {
+      if (rep) st1 += g.stage_stats();
+      continue;
     }
+    if (!g.flush_frames()) throw std::runtime_error("write-behind failed");  // stage 1's files, off the clock
+    if (rep) st1 += g.stage_stats();
+    g.reset_stage_stats();
     // stage 2: "in0 in0 mul" over stage 1's output frame (intermediate-<job>-<node>
     // in herdsman), read from HBM when resident; then every file committed
     const double dt2 = run_all(g, parts, [&](int p) { return task(mid, fin, p, sq); });
@@ -306,6 +307,7 @@ static int bench(int argc, char **argv) {
     if (rep) {
       rates2.push_back(parts * rows / dt2);
       rates2f.push_back(parts * rows / dtf);
+      st2 += g.stage_stats();
     }
   }
   auto summary = [&](const char *what, const std::vector<double> &v) {
@@ -324,8 +326,10 @@ static int bench(int argc, char **argv) {
     std::printf("stage 1:\n");
     print_stages(st1);
     std::printf("stage 2:\n");
+    print_stages(st2);
+  } else {
+    print_stages(st1);
   }
-  print_stages(g.stage_stats());
   return 0;
 }
 

@@ -324,8 +324,8 @@ def _reduce_tree_chunked(o, cts, rlk, mul, chunk, lvl=None):
     qs = o.moduli[:lvl].astype(object)[None, :, None]
 
     def op(x, y):
-        if mul:
-            return o.mul_relin_at(x[None], y[None], rlk, lvl)[0]
+        if mul:  # BFV has no level views: the plain product
+            return (o.mul_relin(x[None], y[None], rlk) if lvl == o.L else o.mul_relin_at(x[None], y[None], rlk, lvl))[0]
         return ((x.astype(object) + y) % qs).astype(np.uint64)
 
     def tree(items):

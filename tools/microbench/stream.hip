@@ -20,7 +20,7 @@ typedef uint64_t u64;
 typedef uint32_t u32;
 
 enum { COL8 = 0, ROW8 = 1, FLAT8 = 2, FLAT16 = 3 };
-enum { COPY = 0, READ = 1, WRITE = 2 };
+enum { COPY = 0, READ = 1, WRITE = 2, READL2 = 3 };  // READL2: the reads cycle over 64 tiles (2 MiB, L2-resident)
 
 template <int PAT>
 __device__ __forceinline__ u32 off_of(u32 tid, u32 blk, int r) {
@@ -100,11 +100,11 @@ __global__ void __launch_bounds__(256) stream_k(const u64 *in, u64 *out, u32 til
   const u32 tid = threadIdx.x;
   u32 t = blockIdx.x;
   if (t >= tiles) return;
-  if constexpr (MODE == READ) {
+  if constexpr (MODE == READ || MODE == READL2) {
     u64 acc = 0;
     for (; t < tiles; t += gridDim.x) {
       T x[NR];
-      tload<PAT, NTL>(x, in, t, tid);
+      tload<PAT, NTL>(x, in, MODE == READL2 ? (t & 63) : t, tid);
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         if constexpr (PAT == FLAT16) acc ^= x[r].a ^ x[r].b;
@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(256) stream_k(const u64 *in, u64 *out, u32 til
 }
 
 static const char *pname[] = {"col8", "row8", "flat8", "flat16"};
-static const char *mname[] = {"copy", "read", "write"};
+static const char *mname[] = {"copy", "read", "write", "readL2"};
 
 template <int PAT, int MODE, bool PIPE, bool NTL, bool NTS>
 void run(u64 *a, u64 *b, u64 *sink, size_t words, bool inplace, u32 wg_per_cu) {
@@ -201,7 +201,17 @@ void sweep(u64 *a, u64 *b, u64 *sink, size_t words) {
   }
 }
 
-int main() {
+// L2-served reads (every workgroup re-reads 64 tiles = 2 MiB): 8-byte against
+// 16-byte accesses per lane, the question for the fused passes' operand loads
+void l2_sweep(u64 *a, u64 *b, u64 *sink, size_t words) {
+  run<FLAT8, READL2, false, false, false>(a, b, sink, words, false, 0);
+  run<FLAT16, READL2, false, false, false>(a, b, sink, words, false, 0);
+  run<ROW8, READL2, false, false, false>(a, b, sink, words, false, 0);
+  run<FLAT8, READL2, false, false, false>(a, b, sink, words, false, 4);
+  run<FLAT16, READL2, false, false, false>(a, b, sink, words, false, 4);
+}
+
+int main(int argc, char **argv) {
   const size_t words = (size_t)4608 * 65536;  // 2.25 GiB: the roofline loop's 4608 limbs
   u64 *a, *b, *sink;
   if (hipMalloc(&a, words * 8) != hipSuccess || hipMalloc(&b, words * 8) != hipSuccess ||
@@ -211,6 +221,10 @@ int main() {
   }
   hipMemset(a, 1, words * 8);
   hipMemset(b, 2, words * 8);
+  if (argc > 1 && argv[1][0] == 'l') {  // ./stream l2
+    l2_sweep(a, b, sink, words);
+    return 0;
+  }
   sweep<FLAT16>(a, b, sink, words);
   sweep<FLAT8>(a, b, sink, words);
   sweep<ROW8>(a, b, sink, words);
