@@ -10,7 +10,8 @@ A call of op_bench is one wave (128 ct-mults); calls are counted by the
 PRO_TENSOR inverse row pass (one per call).  HBM bytes follow
 MI355X_MICROARCH.md: FETCH_SIZE (KB) x 1024 x 2 (gfx950 reports half of a wide
 streaming read), WRITE_SIZE (KB) x 1024.  The input fills (fill_kernel) are
-excluded.
+excluded, and so are the context's table uploads (the runtime's copyBuffer blits
+that run before the first fill: fhe_ctx_create, not the op loop).
 """
 import collections
 import csv
@@ -31,9 +32,11 @@ def short(name):
 def trace(d):
     f = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
     per, calls = collections.defaultdict(lambda: [0, 0.0]), 0
-    for r in csv.DictReader(open(f)):
+    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+    first_fill = next((int(r["Start_Timestamp"]) for r in rows if "fill_kernel" in r["Kernel_Name"]), 0)
+    for r in rows:
         n = r["Kernel_Name"]
-        if "fill_kernel" in n:
+        if "fill_kernel" in n or int(r["Start_Timestamp"]) < first_fill:
             continue
         calls += bool(TENSOR.search(n))
         k = (short(n), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]))
@@ -81,7 +84,7 @@ def main(tdir, fdir, wdir, dst):
         "kernel_TBps": round(tot_b / (tot_ms * 1e-3) / 1e12, 3),
         "dominant": rows[0] if rows else None,
         "kernels": rows,
-        "note": "FETCH_SIZE x 2 (gfx950 half-count of wide streaming reads), WRITE_SIZE as is; fill kernels excluded",
+        "note": "FETCH_SIZE x 2 (gfx950 half-count of wide streaming reads), WRITE_SIZE as is; fill kernels and the context's setup uploads excluded",
     }
     os.makedirs(dst, exist_ok=True)
     json.dump(res, open(os.path.join(dst, "step_summary.json"), "w"), indent=1)
