@@ -19,7 +19,7 @@
 typedef uint64_t u64;
 typedef uint32_t u32;
 
-enum { COL8 = 0, ROW8 = 1, FLAT8 = 2, FLAT16 = 3 };
+enum { COL8 = 0, ROW8 = 1, FLAT8 = 2, FLAT16 = 3, LINE16 = 4 };
 enum { COPY = 0, READ = 1, WRITE = 2, READL2 = 3 };  // READL2: the reads cycle over 64 tiles (2 MiB, L2-resident)
 
 template <int PAT>
@@ -27,7 +27,8 @@ __device__ __forceinline__ u32 off_of(u32 tid, u32 blk, int r) {
   if (PAT == COL8) return (tid / 16 + 16 * r) * 256 + blk * 16 + tid % 16;
   if (PAT == ROW8) return (blk * 16 + tid / 16) * 256 + tid % 16 + 16 * r;
   if (PAT == FLAT8) return blk * 4096 + tid + 256 * r;
-  return blk * 4096 + 2 * (tid + 256 * r);  // FLAT16: word index of a 16-B pair (r < 8)
+  if (PAT == FLAT16) return blk * 4096 + 2 * (tid + 256 * r);  // word index of a 16-B pair (r < 8)
+  return blk * 4096 + 16 * tid + 2 * r;  // LINE16: each lane owns one 128-B line, 8 pairs (a row pass's last-group layout)
 }
 
 struct w2 {
@@ -37,8 +38,9 @@ struct w2 {
 // one tile = 4096 words; NR words (or pairs) per thread
 template <int PAT>
 struct Tile {
-  static constexpr int NR = PAT == FLAT16 ? 8 : 16;
-  typedef typename std::conditional<PAT == FLAT16, w2, u64>::type T;
+  static constexpr bool PAIR = PAT == FLAT16 || PAT == LINE16;
+  static constexpr int NR = PAIR ? 8 : 16;
+  typedef typename std::conditional<PAIR, w2, u64>::type T;
 };
 
 template <int PAT, bool NTL>
@@ -48,7 +50,7 @@ __device__ __forceinline__ void tload(typename Tile<PAT>::T (&x)[Tile<PAT>::NR],
 #pragma unroll
   for (int r = 0; r < Tile<PAT>::NR; ++r) {
     const u32 o = off_of<PAT>(tid, blk, r);
-    if constexpr (PAT == FLAT16) {
+    if constexpr (Tile<PAT>::PAIR) {
       const w2 *p = (const w2 *)(base + o);
       if (NTL) {
         x[r].a = __builtin_nontemporal_load(&p->a);
@@ -69,7 +71,7 @@ __device__ __forceinline__ void tstore(const typename Tile<PAT>::T (&x)[Tile<PAT
 #pragma unroll
   for (int r = 0; r < Tile<PAT>::NR; ++r) {
     const u32 o = off_of<PAT>(tid, blk, r);
-    if constexpr (PAT == FLAT16) {
+    if constexpr (Tile<PAT>::PAIR) {
       w2 *p = (w2 *)(base + o);
       if (NTS) {
         __builtin_nontemporal_store(x[r].a, &p->a);
@@ -86,7 +88,7 @@ __device__ __forceinline__ void tstore(const typename Tile<PAT>::T (&x)[Tile<PAT
 
 template <int PAT>
 __device__ __forceinline__ void bump(typename Tile<PAT>::T &v) {
-  if constexpr (PAT == FLAT16) v.a += 1;
+  if constexpr (Tile<PAT>::PAIR) v.a += 1;
   else v += 1;
 }
 
@@ -107,7 +109,7 @@ __global__ void __launch_bounds__(256) stream_k(const u64 *in, u64 *out, u32 til
       tload<PAT, NTL>(x, in, MODE == READL2 ? (t & 63) : t, tid);
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
-        if constexpr (PAT == FLAT16) acc ^= x[r].a ^ x[r].b;
+        if constexpr (Tile<PAT>::PAIR) acc ^= x[r].a ^ x[r].b;
         else acc ^= x[r];
       }
     }
@@ -116,7 +118,7 @@ __global__ void __launch_bounds__(256) stream_k(const u64 *in, u64 *out, u32 til
     T x[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      if constexpr (PAT == FLAT16) x[r] = w2{tid + (u64)r, (u64)r};
+      if constexpr (Tile<PAT>::PAIR) x[r] = w2{tid + (u64)r, (u64)r};
       else x[r] = tid + (u64)r;
     }
     for (; t < tiles; t += gridDim.x) tstore<PAT, NTS>(x, out, t, tid);
@@ -146,7 +148,7 @@ __global__ void __launch_bounds__(256) stream_k(const u64 *in, u64 *out, u32 til
   }
 }
 
-static const char *pname[] = {"col8", "row8", "flat8", "flat16"};
+static const char *pname[] = {"col8", "row8", "flat8", "flat16", "line16"};
 static const char *mname[] = {"copy", "read", "write", "readL2"};
 
 template <int PAT, int MODE, bool PIPE, bool NTL, bool NTS>
@@ -211,6 +213,21 @@ void l2_sweep(u64 *a, u64 *b, u64 *sink, size_t words) {
   run<FLAT16, READL2, false, false, false>(a, b, sink, words, false, 4);
 }
 
+// a row pass storing straight from its last butterfly group (each lane one
+// 128-B line, 8 x 16-B accesses) against the re-laid-out pair layout
+void line_sweep(u64 *a, u64 *b, u64 *sink, size_t words) {
+  run<LINE16, READ, false, true, false>(a, b, sink, words, false, 0);
+  run<FLAT16, READ, false, true, false>(a, b, sink, words, false, 0);
+  run<LINE16, WRITE, false, false, true>(a, b, sink, words, false, 0);
+  run<FLAT16, WRITE, false, false, true>(a, b, sink, words, false, 0);
+  run<LINE16, WRITE, false, false, false>(a, b, sink, words, false, 0);
+  run<LINE16, COPY, false, true, true>(a, b, sink, words, true, 0);
+  run<FLAT16, COPY, false, true, true>(a, b, sink, words, true, 0);
+  run<LINE16, COPY, false, false, false>(a, b, sink, words, true, 0);
+  run<LINE16, READL2, false, false, false>(a, b, sink, words, false, 0);
+  run<FLAT16, READL2, false, false, false>(a, b, sink, words, false, 0);
+}
+
 int main(int argc, char **argv) {
   const size_t words = (size_t)4608 * 65536;  // 2.25 GiB: the roofline loop's 4608 limbs
   u64 *a, *b, *sink;
@@ -221,6 +238,10 @@ int main(int argc, char **argv) {
   }
   hipMemset(a, 1, words * 8);
   hipMemset(b, 2, words * 8);
+  if (argc > 1 && argv[1][0] == 'r') {  // ./stream row: lane-line against lane-contiguous pairs
+    line_sweep(a, b, sink, words);
+    return 0;
+  }
   if (argc > 1 && argv[1][0] == 'l') {  // ./stream l2
     l2_sweep(a, b, sink, words);
     return 0;
