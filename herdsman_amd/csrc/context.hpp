@@ -190,6 +190,11 @@ struct ConvSrc {
   u64 lift_half;       // 0: plain conversion
   const u64 *lift_sub;  // [nd] device
 };
+// CKKS mul+relin with the tensor product split (EPI_KSQT): the base of the
+// ModDown finish is formed from the ciphertexts a, b [n][2][L][N] themselves
+struct TensorSrc {
+  const u64 *a, *b;
+};
 // Hoisted rotations of few ciphertexts: nr Galois elements' gather passes in
 // one launch (poly p of the batch = rotation p / (2 n), ciphertext poly p % (2 n))
 struct RotBatch {
@@ -201,7 +206,8 @@ struct RotBatch {
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro = nullptr, const u64 *ext = nullptr,
                            const u64 *ksk = nullptr, u32 ndig = 0, u32 base_g = 0, const u64 *pinv = nullptr,
-                           const ConvSrc *pro_src = nullptr, u32 ext_g = 0, const RotBatch *rb = nullptr);
+                           const ConvSrc *pro_src = nullptr, u32 ext_g = 0, const RotBatch *rb = nullptr,
+                           const TensorSrc *tsrc = nullptr);
 // ModUp of digit j fused into the column pass of the forward NTT of its
 // converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
@@ -215,7 +221,10 @@ int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32
                        bool all_limbs = false, const RotBatch *rb = nullptr);
 // (base null: sigma(c0) is not stored; the combine then reads it with base_g)
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
-int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig);
+// d2_only (PRO_TENSOR2, two-pass sizes): out is not written; the ModDown
+// finish forms d0 and d1 (ntt_fwd_combine_launch with a TensorSrc)
+int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig,
+                          bool d2_only = false);
 // RNS kernels (rns.hip)
 enum class EwOp { Add, Sub, Mul };
 int ew_launch(fhe_ctx *c, EwOp op, const u64 *a, const u64 *b, u64 *out, u32 n_polys, u32 mod_begin, u32 n_limbs);

@@ -104,6 +104,7 @@ struct NttArgs {
   // here instead of being read): acc[p][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1,
   // p = 2 ct + b, with ext [ct][e_ndig][e_QP][N] and ksk [e_ndig][2][e_QP][N]
   const u64 *e_ext, *e_ksk;
+  const u64 *e_ta, *e_tb;  // EPI_KSQT: the operands a, b [ct][2][L][N] of the tensor product (the base)
   u32 e_ndig, e_QP;
   u32 e_kQP, e_kshift;  // key rows per digit half; key row of limb i >= L is i + e_kshift (level views)
   u32 e_ext_g;          // EPI_KSQG / PRO_KSPG: ext is read as sigma_g(ext) (hoisted rotation)
@@ -170,13 +171,23 @@ namespace {
 // EPI_KSQG / PRO_KSPG + d - 1: the same with the ext words gathered through
 // sigma_g (NttArgs::e_ext_g): the inner product of a hoisted rotation, whose
 // one ModUp of c1 serves every Galois element
-enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, EPI_KSQ = 6, PRO_CONV = 11,
-       PRO_KSP = 16, EPI_KSQG = 21, PRO_KSPG = 26 };
+// PRO_TENSOR2 / EPI_KSQT + d - 1: CKKS mul+relin with the tensor product split
+// between the two ends of the key switch: the INTT(d2) prologue forms d2 = a1 b1
+// only, and the ModDown finish forms its base d0 = a0 b0 (b = 0) or
+// d1 = a0 b1 + a1 b0 (b = 1) from a and b itself, so d0 and d1 never reach HBM
+enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, PRO_TENSOR2 = 5, EPI_KSQ = 6,
+       PRO_CONV = 11, PRO_KSP = 16, EPI_KSQG = 21, PRO_KSPG = 26, EPI_KSQT = 31 };
+__host__ __device__ constexpr bool is_tensor(int e) { return e == PRO_TENSOR || e == PRO_TENSOR2; }
+__host__ __device__ constexpr bool ksq_tensor(int e) { return e >= EPI_KSQT && e < EPI_KSQT + 4; }
 __host__ __device__ constexpr bool is_conv(int e) { return e >= PRO_CONV && e < PRO_CONV + 4; }
 __host__ __device__ constexpr int conv_ns(int e) { return e - PRO_CONV + 1; }
 __host__ __device__ constexpr bool ksq_gather(int e) { return e >= EPI_KSQG && e < EPI_KSQG + 4; }
-__host__ __device__ constexpr bool is_ksq(int e) { return (e >= EPI_KSQ && e < EPI_KSQ + 4) || ksq_gather(e); }
-__host__ __device__ constexpr int ksq_digits(int e) { return e - (ksq_gather(e) ? EPI_KSQG : EPI_KSQ) + 1; }
+__host__ __device__ constexpr bool is_ksq(int e) {
+  return (e >= EPI_KSQ && e < EPI_KSQ + 4) || ksq_gather(e) || ksq_tensor(e);
+}
+__host__ __device__ constexpr int ksq_digits(int e) {
+  return e - (ksq_gather(e) ? EPI_KSQG : ksq_tensor(e) ? EPI_KSQT : EPI_KSQ) + 1;
+}
 __host__ __device__ constexpr bool is_combine(int e) { return e == EPI_COMBINE || is_ksq(e); }
 __host__ __device__ constexpr bool ksp_gather(int e) { return e >= PRO_KSPG && e < PRO_KSPG + 4; }
 __host__ __device__ constexpr bool is_ksp(int e) { return (e >= PRO_KSP && e < PRO_KSP + 4) || ksp_gather(e); }
@@ -206,7 +217,7 @@ struct EpiRow {
   u64 *o0, *o1, *ext;
   u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base or null; ext); combine: e_g
   u32 xg;  // EPI_KSQG / PRO_KSPG: the Galois element ext is gathered through
-  u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is
+  u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is; EPI_KSQT: b
   const u64 *src;  // PRO_CONV: source limb 0 of this poly (limb i at src + i N)
   u64 h[4];        // PRO_CONV: h[i][m] of this workgroup's target limb
   u64 lift_sub;    // PRO_CONV, one source, rescale lift: q_l mod q_m
@@ -509,8 +520,9 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     // last group computes (the LDS footprint caps occupancy at 4 waves per
     // SIMD, so the 128-VGPR budget has room for them)
     constexpr int RE = is_combine(EPI) ? R : 1;
+    constexpr int RB = is_combine(EPI) && !ksq_tensor(EPI) ? R : 1;  // EPI_KSQT forms its base in the store loop
     using IO = IoL<S, LOGR>;
-    u64 pa[RE], pb[RE];
+    u64 pa[RE], pb[RB];
     if constexpr (is_combine(EPI)) {
 #pragma unroll
       for (int r = 0; r < R; r += IO::STEP) {
@@ -520,7 +532,8 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
             const u64x2 v = ld2_b(ep.acc + kr, voff);
             pa[r] = v.x, pa[r + 1] = v.y;
           }
-          if (!ep.add) {
+          if constexpr (ksq_tensor(EPI)) {
+          } else if (!ep.add) {
             pb[r] = pb[r + 1] = 0;
           } else if (ep.g) {  // sigma_g(base): a gather, word by word
             pb[r] = ld_b(ep.base, aut_src<LOG_N>((voff >> 3) + kr, ep.g));
@@ -531,7 +544,8 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
           }
         } else {
           if constexpr (EPI == EPI_COMBINE) pa[r] = ld_b(ep.acc + kr, voff);
-          if (!ep.add) pb[r] = 0;
+          if constexpr (ksq_tensor(EPI)) {
+          } else if (!ep.add) pb[r] = 0;
           else if (ep.g) pb[r] = ld_b(ep.base, aut_src<LOG_N>((voff >> 3) + kr, ep.g));  // sigma_g(base)
           else pb[r] = ld_b(ep.base + kr, voff);
         }
@@ -605,84 +619,133 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
           }
         }
       };
-      if constexpr (is_ksq(EPI)) {
+      // EPI_KSQT: the tensor operands of the base, (a0, b0) for b = 0 and
+      // (a0, a1, b0, b1) for b = 1 (TM = 1, 2), loaded in the step that uses them.
+      // A ring of them beside the key-switching one took the pass past 128 VGPRs
+      // (one step ahead: no faster, profiles/r05/ab_tensor_split.txt).  The b = 1
+      // workgroup follows the b = 0 one on the same XCD (the remap in ntt_pass),
+      // so its a0, b0 come mostly from L2.
+      constexpr int NTO = ksq_tensor(EPI) ? 4 : 1;
+      const auto tfetch = [&](auto tm, int st, u64 (&slot)[NTO][ST]) {
+        constexpr int TM = decltype(tm)::value;
+        if constexpr (TM != 0) {
+          const u32 kr = IO::k_reg(st * ST);
+          const u64 *src[4] = {ep.a0, ep.a1, ep.b0, ep.b1};
 #pragma unroll
-        for (int st = 0; st < PDS; ++st) fetch(st, ek[st]);
-      }
-      // row pass ending in a group whose lanes each own contiguous words:
-      // re-layout through LDS so the HBM store is coalesced (the IO layout)
-      const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
-#pragma unroll
-      for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + lds_pad(GP::k_reg(r))] = x[r];
-      __syncthreads();
-      const u32 lr = lds_idx<S>(w, IO::k_thr(ts));
-#pragma unroll
-      for (int st = 0; st < NST; ++st) {
-        if constexpr (is_ksq(EPI)) {
-          if (st + PDS < NST) fetch(st + PDS, ek[(st + PDS) % (PDS + 1)]);
-        }
-        u64 o[ST];
-#pragma unroll
-        for (int h = 0; h < ST; ++h) {
-          const int r = st * ST + h;
-          const u32 kr = IO::k_reg(r);
-          const u64 v = lds[lr + kr + lds_pad(kr)];
-          if constexpr (is_combine(EPI)) {
-            // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM.
-            // acc - conv is formed as acc + Bq - v (v < Bq, B = 4 WIDE / 2): below
-            // 5q < 2^63 for q < 2^60 and 3q < 2^63 for q < 2^61, inside the
-            // Montgomery input bound, whose product below 1.5q (2q generic)
-            // is canonicalised by one conditional subtraction
-            u64 acc;
-            if constexpr (is_ksq(EPI)) {
-              // acc_Q = sum_j ext_j ksk_j R^-1 (ext carries R), at the store
-              // position: acc_Q never makes an HBM round trip.  Each product is
-              // below 1.5q (2q generic), so one subtraction of 4q (WIDE) leaves
-              // the lazy sum below 4q; otherwise it is made canonical.
-              u64 e[KD], k[KD], pr[KD];
-#pragma unroll
-              for (int j = 0; j < KD; ++j) {
-                e[j] = ek[st % (PDS + 1)][j][h];
-                k[j] = ek[st % (PDS + 1)][KD + j][h];
-              }
-              if constexpr (SP) {
-                mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
-              } else if constexpr (GEN_VEC) {
-                mont_mul_gen_vec<KD>(pr, e, k, mi);
-              } else {
-#pragma unroll
-                for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
-              }
-              acc = pr[0];
-              if constexpr (WIDE) {
-                // q < 2^60: the whole sum stays below 6q < 2^63
-#pragma unroll
-                for (int j = 1; j < KD; ++j) acc += pr[j];
-                if constexpr (KD > 2) acc = harvey_csub(acc, nq4);
-              } else {
-                // q < 2^61: keep the running sum below 2q, then canonical
-#pragma unroll
-                for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
-                acc = harvey_csub(acc, nq1);
-              }
+          for (int i = 0; i < 4; ++i) {
+            if (TM == 1 && (i & 1)) continue;
+            if constexpr (ST == 2) {
+              const u64x2 v2 = ld2_b(src[i] + kr, voff);
+              slot[i][0] = v2.x, slot[i][1] = v2.y;
             } else {
-              acc = pa[r];
+              slot[i][0] = ld_b(src[i] + kr, voff);
             }
-            u64 ks = harvey_csub(mont_mul<SP>((acc + cb1) + ~v, ep.pinv, mi), nq1);
-            if (ep.add) ks = add_mod(ks, pb[r], q);
-            o[h] = ks;
-          } else {
-            o[h] = v;
           }
         }
-        const u32 ko = IO::k_reg(st * ST);
-        if constexpr (ST == 2) {
-          if constexpr (is_combine(EPI)) st2_e(ep.out + ko, voff, u64x2{o[0], o[1]});
-          else st2_d(data + ko, voff, u64x2{o[0], o[1]});
-        } else {
-          if constexpr (is_combine(EPI)) st_e(ep.out + ko, voff, o[0]);
-          else st_d(data + ko, voff, o[0]);
+      };
+      const auto store_rows = [&](auto tm) {
+        constexpr int TM = decltype(tm)::value;
+        if constexpr (is_ksq(EPI)) {
+#pragma unroll
+          for (int st = 0; st < PDS; ++st) fetch(st, ek[st]);
         }
+        // row pass ending in a group whose lanes each own contiguous words:
+        // re-layout through LDS so the HBM store is coalesced (the IO layout)
+        const u32 lw = lds_idx<S>(w, GP::k_thr(ts));
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[lw + GP::k_reg(r) + lds_pad(GP::k_reg(r))] = x[r];
+        __syncthreads();
+        const u32 lr = lds_idx<S>(w, IO::k_thr(ts));
+#pragma unroll
+        for (int st = 0; st < NST; ++st) {
+          if constexpr (is_ksq(EPI)) {
+            if (st + PDS < NST) fetch(st + PDS, ek[(st + PDS) % (PDS + 1)]);
+          }
+          u64 t[NTO][ST];
+          tfetch(tm, st, t);
+          u64 o[ST];
+#pragma unroll
+          for (int h = 0; h < ST; ++h) {
+            const int r = st * ST + h;
+            const u32 kr = IO::k_reg(r);
+            const u64 v = lds[lr + kr + lds_pad(kr)];
+            if constexpr (is_combine(EPI)) {
+              // ModDown finish fused into the last pass of NTT(conv): conv never reaches HBM.
+              // acc - conv is formed as acc + Bq - v (v < Bq, B = 4 WIDE / 2): below
+              // 5q < 2^63 for q < 2^60 and 3q < 2^63 for q < 2^61, inside the
+              // Montgomery input bound, whose product below 1.5q (2q generic)
+              // is canonicalised by one conditional subtraction
+              u64 acc;
+              if constexpr (is_ksq(EPI)) {
+                // acc_Q = sum_j ext_j ksk_j R^-1 (ext carries R), at the store
+                // position: acc_Q never makes an HBM round trip.  Each product is
+                // below 1.5q (2q generic), so one subtraction of 4q (WIDE) leaves
+                // the lazy sum below 4q; otherwise it is made canonical.
+                u64 e[KD], k[KD], pr[KD];
+#pragma unroll
+                for (int j = 0; j < KD; ++j) {
+                  e[j] = ek[st % (PDS + 1)][j][h];
+                  k[j] = ek[st % (PDS + 1)][KD + j][h];
+                }
+                if constexpr (SP) {
+                  mont_mul_sp_vec<KD>(pr, e, k, mi.q_hi);
+                } else if constexpr (GEN_VEC) {
+                  mont_mul_gen_vec<KD>(pr, e, k, mi);
+                } else {
+#pragma unroll
+                  for (int j = 0; j < KD; ++j) pr[j] = mont_mul<SP>(e[j], k[j], mi);
+                }
+                acc = pr[0];
+                if constexpr (WIDE) {
+                  // q < 2^60: the whole sum stays below 6q < 2^63
+#pragma unroll
+                  for (int j = 1; j < KD; ++j) acc += pr[j];
+                  if constexpr (KD > 2) acc = harvey_csub(acc, nq4);
+                } else {
+                  // q < 2^61: keep the running sum below 2q, then canonical
+#pragma unroll
+                  for (int j = 1; j < KD; ++j) acc = harvey_csub(acc + pr[j], nq2);
+                  acc = harvey_csub(acc, nq1);
+                }
+              } else {
+                acc = pa[r];
+              }
+              u64 ks = harvey_csub(mont_mul<SP>((acc + cb1) + ~v, ep.pinv, mi), nq1);
+              if constexpr (TM != 0) {
+                // the base of this poly from the ciphertexts: d0 = a0 b0, d1 = a0 b1 + a1 b0
+                u64 bv;
+                if constexpr (TM == 1) {
+                  bv = mul_mod<SP>(t[0][h], t[2][h], mi);
+                } else {
+                  U128 sm = mul128(t[0][h], t[3][h]);
+                  mac128(sm, t[1][h], t[2][h]);
+                  bv = reduce128<SP>(sm, mi);
+                }
+                ks = add_mod(ks, bv, q);
+              } else if (ep.add) {
+                ks = add_mod(ks, pb[r], q);
+              }
+              o[h] = ks;
+            } else {
+              o[h] = v;
+            }
+          }
+          const u32 ko = IO::k_reg(st * ST);
+          if constexpr (ST == 2) {
+            if constexpr (is_combine(EPI)) st2_e(ep.out + ko, voff, u64x2{o[0], o[1]});
+            else st2_d(data + ko, voff, u64x2{o[0], o[1]});
+          } else {
+            if constexpr (is_combine(EPI)) st_e(ep.out + ko, voff, o[0]);
+            else st_d(data + ko, voff, o[0]);
+          }
+        }
+      };
+      using T0 = std::integral_constant<int, 0>;
+      if constexpr (ksq_tensor(EPI)) {
+        if (ep.e == 0) store_rows(std::integral_constant<int, 1>{});
+        else store_rows(std::integral_constant<int, 2>{});
+      } else {
+        store_rows(T0{});
       }
     } else {
       static_assert(!is_combine(EPI), "epilogues run in the re-laid-out row store");
@@ -719,20 +782,23 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
     using GZ = IoL<S, LOGR, PAIR_IO && !is_ksp(EPI)>;
     constexpr int ST = GZ::STEP;
     voff = (gb + GZ::k_thr(ts)) << 3;
-    if constexpr (EPI == PRO_TENSOR) {
-      // the CKKS tensor formulas, element-wise at the coalesced positions.
+    if constexpr (is_tensor(EPI)) {
+      // the CKKS tensor formulas, element-wise at the coalesced positions
+      // (PRO_TENSOR2: d2 only; EPI_KSQT forms d0 and d1).
       // Software-pipelined PD steps deep: the operand loads of step s + PD
       // are issued before step s's stores (the outputs may alias the
       // operands element-wise only, so the compiler would otherwise wait for
       // each step's loads right after the previous step's stores)
       constexpr int PD = SP ? (ST == 2 ? 1 : 2) : 0;  // the generic products need the registers
       constexpr int NST = R / ST;
-      u64 op[PD + 1][4][ST];
-      const auto fetch = [&](int st, u64 (&o)[4][ST]) {
+      constexpr bool ALL = EPI == PRO_TENSOR;
+      constexpr int NO = ALL ? 4 : 2;  // operand streams: (a0, a1, b0, b1) or (a1, b1)
+      u64 op[PD + 1][NO][ST];
+      const auto fetch = [&](int st, u64 (&o)[NO][ST]) {
         const u32 kn = GZ::k_reg(st * ST);
-        const u64 *src[4] = {ep.a0, ep.a1, ep.b0, ep.b1};
+        const u64 *src[4] = {ALL ? ep.a0 : ep.a1, ALL ? ep.a1 : ep.b1, ep.b0, ep.b1};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NO; ++i) {
           if constexpr (ST == 2) {
             const u64x2 v = ld2_b(src[i] + kn, voff);
             o[i][0] = v.x, o[i][1] = v.y;
@@ -749,24 +815,30 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         u64 o0[ST], o1[ST], oe[ST];
 #pragma unroll
         for (int h = 0; h < ST; ++h) {
-          const u64 a0 = op[st % (PD + 1)][0][h], a1 = op[st % (PD + 1)][1][h];
-          const u64 b0 = op[st % (PD + 1)][2][h], b1 = op[st % (PD + 1)][3][h];
-          o0[h] = mul_mod<SP>(a0, b0, mi);
-          U128 sm = mul128(a0, b1);
-          mac128(sm, a1, b0);
-          o1[h] = reduce128<SP>(sm, mi);
+          const u64 a1 = op[st % (PD + 1)][ALL ? 1 : 0][h], b1 = op[st % (PD + 1)][ALL ? 3 : 1][h];
+          if constexpr (ALL) {
+            const u64 a0 = op[st % (PD + 1)][0][h], b0 = op[st % (PD + 1)][2][h];
+            o0[h] = mul_mod<SP>(a0, b0, mi);
+            U128 sm = mul128(a0, b1);
+            mac128(sm, a1, b0);
+            o1[h] = reduce128<SP>(sm, mi);
+          }
           const u64 t = mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi);  // d2 in [0, 2q)
           x[st * ST + h] = csub(t, mi.q);
           oe[h] = csub(mont_mul<SP>(t, mi.r2, mi), mi.q);  // d2 R
         }
         const u32 kr = GZ::k_reg(st * ST);
         if constexpr (ST == 2) {
-          st2_e(ep.o0 + kr, voff, u64x2{o0[0], o0[1]});
-          st2_e(ep.o1 + kr, voff, u64x2{o1[0], o1[1]});
+          if constexpr (ALL) {
+            st2_e(ep.o0 + kr, voff, u64x2{o0[0], o0[1]});
+            st2_e(ep.o1 + kr, voff, u64x2{o1[0], o1[1]});
+          }
           st2_e(ep.ext + kr, voff, u64x2{oe[0], oe[1]});
         } else {
-          st_e(ep.o0 + kr, voff, o0[0]);
-          st_e(ep.o1 + kr, voff, o1[0]);
+          if constexpr (ALL) {
+            st_e(ep.o0 + kr, voff, o0[0]);
+            st_e(ep.o1 + kr, voff, o1[0]);
+          }
           st_e(ep.ext + kr, voff, oe[0]);
         }
       }
@@ -1100,17 +1172,17 @@ int launch_persist(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
 // The tensor prologue asks for 4 waves per SIMD (the LDS allows 4 workgroups
 // per CU anyway), so its 16-byte operand pairs stay within 128 VGPRs
 __host__ __device__ constexpr int pass_min_waves(int EPI, bool SP, int threads) {
-  return threads != 256 ? 1 : (PAIR_IO && EPI == PRO_TENSOR && SP) ? 4 : NTT_MINW;
+  return threads != 256 ? 1 : (PAIR_IO && (is_tensor(EPI) || ksq_tensor(EPI)) && SP) ? 4 : NTT_MINW;
 }
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int WM>
 __global__ void __launch_bounds__(W << (S - LOGR), pass_min_waves(EPI, SP, W << (S - LOGR)))
     ntt_pass(NttArgs a) {
-  static_assert(is_combine(EPI) || EPI == EPI_NONE || EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH ||
+  static_assert(is_combine(EPI) || EPI == EPI_NONE || is_tensor(EPI) || EPI == PRO_AUTOMORPH ||
                     EPI == PRO_BFVT || is_conv(EPI) || is_ksp(EPI),
                 "ntt_pass epilogues");
   static_assert(!is_conv(EPI) || (!INV && COLS), "the conversion prologue feeds a forward column pass");
   static_assert(!is_combine(EPI) || (!INV && !COLS), "epilogues follow a forward row pass");
-  static_assert((EPI != PRO_TENSOR && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT && !is_ksp(EPI)) || (INV && !COLS),
+  static_assert((!is_tensor(EPI) && EPI != PRO_AUTOMORPH && EPI != PRO_BFVT && !is_ksp(EPI)) || (INV && !COLS),
                 "prologues feed an inverse row pass");
   using PG = PassGeo<LOG_N, S, COLS, INV>;
   static_assert(!is_combine(EPI) || PG::LAST, "epilogues run in the last pass");
@@ -1228,8 +1300,18 @@ __global__ void __launch_bounds__(W << (S - LOGR), pass_min_waves(EPI, SP, W << 
     ep.pinv = a.e_pinv[limb];
     ep.add = (a.e_add_mask >> (poly & 1)) & 1;
     ep.g = ksq_gather(EPI) && a.e_rp ? a.e_g_r[rot] : a.e_g;
+    if constexpr (ksq_tensor(EPI)) {
+      // this poly's ciphertext (ct, b) = (cpoly / 2, cpoly % 2): a_j, b_j at (2 ct + j, limb)
+      const size_t LN = (size_t)a.map.poly_stride << LOG_N;
+      const size_t o = (((size_t)(cpoly & ~1u) * a.map.poly_stride + limb) << LOG_N);
+      ep.a0 = a.e_ta + o;
+      ep.a1 = ep.a0 + LN;
+      ep.b0 = a.e_tb + o;
+      ep.b1 = ep.b0 + LN;
+      ep.e = cpoly & 1;
+    }
   }
-  if constexpr (EPI == PRO_TENSOR) {
+  if constexpr (is_tensor(EPI)) {
     const size_t LN = (size_t)a.t_L << LOG_N;
     const size_t o = ((size_t)poly * 2 * a.t_L + limb) << LOG_N;
     ep.a0 = a.t_a + o;
@@ -1317,7 +1399,7 @@ int launch_pass(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
     if (inv) return fhe_fail(c, FHE_ERR_INVALID, "ntt epilogue on an inverse pass");
     return c->special ? launch_fwd<LOG_N, S, W, COLS, EPI, true>(c, a, n_jobs)
                       : launch_fwd<LOG_N, S, W, COLS, EPI, false>(c, a, n_jobs);
-  } else if constexpr (EPI == PRO_TENSOR || EPI == PRO_AUTOMORPH || EPI == PRO_BFVT || is_ksp(EPI)) {
+  } else if constexpr (is_tensor(EPI) || EPI == PRO_AUTOMORPH || EPI == PRO_BFVT || is_ksp(EPI)) {
     if (!inv) return fhe_fail(c, FHE_ERR_INVALID, "prologue on a forward pass");
     return c->special ? launch_one<LOG_N, S, W, COLS, true, true, EPI>(c, a, n_jobs)
                       : launch_one<LOG_N, S, W, COLS, true, false, EPI>(c, a, n_jobs);

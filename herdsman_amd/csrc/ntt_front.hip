@@ -6,9 +6,12 @@
 // CKKS mul+relin front end: the tensor product fused into the first pass of
 // the inverse NTT of d2 (PRO_TENSOR).  a, b, out: [n][2][L][N] (out may alias
 // a or b); dc [n][L][N] receives INTT(d2); ext's own-digit slots receive d2 R.
-int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig) {
+// d2_only: out is left alone (PRO_TENSOR2: only a1 and b1 are read).
+int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig,
+                          bool d2_only) {
   const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
+  if (d2_only && c->log_n <= 14) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "split tensor product: log_n");
   const u32 per = TENSOR_CHUNK;  // ciphertexts per pass pair (gridDim.y <= 65535)
   for (u32 p0 = 0; p0 < n; p0 += per) {
     const u32 np = std::min(per, n - p0);
@@ -35,7 +38,8 @@ int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 
     if (c->log_n <= 14) {
       rc = single_pass<PRO_TENSOR>(c, t, true, n_jobs);
     } else {
-      if ((rc = row_pass<PRO_TENSOR>(c, t, true, n_jobs))) return rc;
+      if ((rc = d2_only ? row_pass<PRO_TENSOR2>(c, t, true, n_jobs) : row_pass<PRO_TENSOR>(c, t, true, n_jobs)))
+        return rc;
       rc = ntt_col_plain(c, t, true, n_jobs);
     }
     if (rc) return rc;

@@ -11,13 +11,17 @@
 // forms acc[2 ct + b][i] = sum_j ext[ct][j][i] ksk[j][b][i] R^-1 itself.
 int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u32 acc_stride, const u64 *base,
                            u64 *out, u32 add_mask, const ConvTab *pro, const u64 *ext, const u64 *ksk, u32 ndig,
-                           u32 base_g, const u64 *pinv, const ConvSrc *pro_src, u32 ext_g, const RotBatch *rb) {
+                           u32 base_g, const u64 *pinv, const ConvSrc *pro_src, u32 ext_g, const RotBatch *rb,
+                           const TensorSrc *tsrc) {
   const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
   if (ext && (c->log_n <= 14 || ndig > 4 || (n_polys & 1)))
     return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch inner product: log_n / digits");
   if (base_g && c->log_n <= 14) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated combine base: log_n");
   if ((ext_g || rb) && !ext) return fhe_fail(c, FHE_ERR_INVALID, "gathered ext without the fused inner product");
+  // tsrc: the base is formed from the ciphertexts (EPI_KSQT), added to both polys
+  if (tsrc && (!ext || ext_g || rb || base_g || add_mask != 3u))
+    return fhe_fail(c, FHE_ERR_INVALID, "split tensor product: plain fused inner product only");
   // rb: the n_polys = 2 n nr polys of rb->nr rotations in one chunk; base (the
   // ciphertexts, read through each rotation's sigma_g) has 2 n polys
   if (rb && (rb->nr < 1 || rb->nr > FHE_ROT_BATCH || n_polys > COMBINE_CHUNK || n_polys % (2 * rb->nr)))
@@ -44,6 +48,10 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
       a.e_ndig = ndig;
       a.e_QP = QP;
       a.e_kQP = ctx_key_qp(c);
+      if (tsrc) {
+        a.e_ta = tsrc->a + (size_t)p0 * L * N;  // poly p0 = 2 ct: ciphertext ct's a_0
+        a.e_tb = tsrc->b + (size_t)p0 * L * N;
+      }
       a.e_ext_g = ext_g & ((2u << c->log_n) - 1);
       if (rb) {
         a.e_rp = n_polys / rb->nr;
@@ -81,7 +89,11 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
         rc = ntt_col_plain(c, a, false, n_jobs);
       }
       if (rc) return rc;
-      switch (ext ? ndig + (ext_g || rb ? 4 : 0) : 0) {
+      switch (ext ? ndig + (ext_g || rb ? 4 : 0) + (tsrc ? 8 : 0) : 0) {
+        case 9: rc = row_pass<EPI_KSQT>(c, a, false, n_jobs); break;
+        case 10: rc = row_pass<EPI_KSQT + 1>(c, a, false, n_jobs); break;
+        case 11: rc = row_pass<EPI_KSQT + 2>(c, a, false, n_jobs); break;
+        case 12: rc = fhe_fail(c, FHE_ERR_UNSUPPORTED, "split tensor product: 4 digits"); break;  // spills
         case 5: rc = row_pass<EPI_KSQG>(c, a, false, n_jobs); break;
         case 6: rc = row_pass<EPI_KSQG + 1>(c, a, false, n_jobs); break;
         case 7: rc = row_pass<EPI_KSQG + 2>(c, a, false, n_jobs); break;

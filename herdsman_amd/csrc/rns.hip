@@ -952,6 +952,13 @@ struct KsWs {
 #ifndef KSP_FUSE
 #define KSP_FUSE 1  // the P limbs' inner product inside INTT(acc_P)'s first pass (0: ks_inner_kernel)
 #endif
+#ifndef TENSOR_SPLIT
+#define TENSOR_SPLIT 1  // CKKS mul+relin: d0, d1 formed in the ModDown finish (ckks_mul_relin_impl)
+#endif
+static bool ranges_overlap(const u64 *x, const u64 *y, size_t bytes) {
+  const char *p = (const char *)x, *q = (const char *)y;
+  return p < q + bytes && q < p + bytes;
+}
 static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
   const size_t L = c->L, QP = c->L + c->K, N = c->n;
   KsWs w;
@@ -1009,7 +1016,7 @@ static bool ks_fused_inner(const fhe_ctx *c, u32 ndig, bool ntt_form) {
   return ntt_form && c->fuse_moddown && ndig <= 4 && KSP_FUSE;
 }
 static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, const u64 *base, u64 *out, u32 n,
-                     u32 add_mask, bool ntt_form, u32 base_g, u32 ext_g) {
+                     u32 add_mask, bool ntt_form, u32 base_g, u32 ext_g, const TensorSrc *tsrc = nullptr) {
   const u32 L = c->L, K = c->K, QP = L + K, N = c->n, ndig = w.ndig;
   u64 *acc = w.acc, *conv = w.conv;
   int rc;
@@ -1032,8 +1039,9 @@ static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, 
     if (ksq && KSP_FUSE) rc = ntt_inv_ksp_launch(c, acc, ext, ksk, n, ndig, ext_g);
     else rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale);
     if (rc) return rc;
+    if (tsrc && !(ksq && KSP_FUSE)) return fhe_fail(c, FHE_ERR_INVALID, "split tensor product without EPI_KSQ");
     return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, &c->moddown, ksq ? ext : nullptr,
-                                  ksk, ndig, base_g, nullptr, nullptr, ext_g);
+                                  ksk, ndig, base_g, nullptr, nullptr, ext_g, nullptr, tsrc);
   }
   if (base_g) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated key-switch base without the fused ModDown");
   // 5. ModDown: INTT the P part (all of Q u P for BFV), convert P -> Q
@@ -1047,9 +1055,9 @@ static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, 
 }
 
 static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
-                         bool ntt_form, bool dc_is_coef = false, u32 base_g = 0) {
+                         bool ntt_form, bool dc_is_coef = false, u32 base_g = 0, const TensorSrc *tsrc = nullptr) {
   int rc = ks_extend(c, w, n, ntt_form, dc_is_coef);
-  return rc ? rc : ks_finish(c, w, w.ext, ksk, base, out, n, add_mask, ntt_form, base_g, 0);
+  return rc ? rc : ks_finish(c, w, w.ext, ksk, base, out, n, add_mask, ntt_form, base_g, 0, tsrc);
 }
 
 template <bool SP>
@@ -1131,13 +1139,22 @@ int keyswitch_ex(fhe_ctx *c, const u64 *d, u32 d_stride, const u64 *ksk, const u
 
 // CKKS ct x ct: the tensor product (and the KS preparation of d2) runs inside
 // the first pass of INTT(d2) (ntt.hip PRO_TENSOR), then relinearise.
+// At two-pass sizes with the fused inner product the tensor product is split
+// (TENSOR_SPLIT): d2 = a1 b1 in INTT(d2)'s first pass (PRO_TENSOR2) and the
+// base d0, d1 in the ModDown finish (EPI_KSQT), so d0 and d1 never make an HBM
+// round trip.  The finish reads a and b after other workgroups have written
+// out, so out must not overlap them; an aliased call takes the unsplit path.
 int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u64 *out, u32 n) {
   void *ws;
   int rc = ctx_workspace(c, keyswitch_ws_bytes(c, n), &ws);
   if (rc) return rc;
   const KsWs w = ks_layout(c, n, (u64 *)ws);
-  if ((rc = ntt_inv_tensor_launch(c, a, b, out, w.dc, w.ext, n, w.ndig))) return rc;
-  return keyswitch_run(c, w, rlk, out, out, n, 3u, true, true);
+  const size_t bytes = sizeof(u64) * 2 * c->L * c->n * (size_t)n;
+  const bool split = TENSOR_SPLIT && c->log_n > 14 && c->fuse_moddown && w.ndig <= 3 && KSP_FUSE &&
+                     !ranges_overlap(out, a, bytes) && !ranges_overlap(out, b, bytes);
+  if ((rc = ntt_inv_tensor_launch(c, a, b, out, w.dc, w.ext, n, w.ndig, split))) return rc;
+  const TensorSrc ts{a, b};
+  return keyswitch_run(c, w, rlk, out, out, n, 3u, true, true, 0, split ? &ts : nullptr);
 }
 
 // Rotation: automorphism (fused with the KS preparation of sigma(c1)) + KS.

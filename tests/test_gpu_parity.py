@@ -161,7 +161,9 @@ def test_ckks_golden(hb):
 def test_ckks_mul_relin_vs_oracle(hb, log_n, L, K, dnum, n_ct):
     """(16, 12, 4, 3) is the BASELINE metric config (ct-mult+relin, N=2^16, L=12).
     log_n 15..17 run the two-pass NTT whose last pass carries the fused ModDown finish
-    (ragged digits at 15)."""
+    (ragged digits at 15).  There the call with a separate output splits the tensor
+    product (d2 in INTT(d2)'s first pass, d0 / d1 in the ModDown finish: PRO_TENSOR2 +
+    EPI_KSQT); the in-place call takes the unsplit path (ckks_mul_relin_impl)."""
     o, c = pair(hb, SCHEME_CKKS, log_n, L, K, dnum)
     a = o.uniform((n_ct, 2, L, 1 << log_n), seed=10)
     b = o.uniform((n_ct, 2, L, 1 << log_n), seed=11)

@@ -21,7 +21,7 @@ import os
 import re
 import sys
 
-TENSOR = re.compile(r"true, false, true, 2(, \d)?>")
+TENSOR = re.compile(r"true, false, true, [25](, \d)?>")  # PRO_TENSOR or PRO_TENSOR2
 
 
 def short(name):
