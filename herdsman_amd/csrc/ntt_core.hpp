@@ -35,6 +35,9 @@
 
 #include "context.hpp"
 
+#ifndef KSQT_MINW
+#define KSQT_MINW 3  // EPI_KSQT (special moduli) minimum waves per SIMD (4: 128 VGPRs, spills, -1.5%)
+#endif
 #ifndef KSQ_PD
 #define KSQ_PD 2  // EPI_KSQ operand prefetch depth (elements; 3 measured no faster, profiles/r03/ab_ksq_pd_aut.txt)
 #endif
@@ -174,7 +177,8 @@ namespace {
 // PRO_TENSOR2 / EPI_KSQT + d - 1: CKKS mul+relin with the tensor product split
 // between the two ends of the key switch: the INTT(d2) prologue forms d2 = a1 b1
 // only, and the ModDown finish forms its base d0 = a0 b0 (b = 0) or
-// d1 = a0 b1 + a1 b0 (b = 1) from a and b itself, so d0 and d1 never reach HBM
+// d1 = a0 b1 + a1 b0 (b = 1) from a and b itself, and the own digit's ext word
+// d2 R as well, so d0, d1 and d2 R never reach HBM
 enum { EPI_NONE = 0, EPI_COMBINE = 1, PRO_TENSOR = 2, PRO_AUTOMORPH = 3, PRO_BFVT = 4, PRO_TENSOR2 = 5, EPI_KSQ = 6,
        PRO_CONV = 11, PRO_KSP = 16, EPI_KSQG = 21, PRO_KSPG = 26, EPI_KSQT = 31 };
 __host__ __device__ constexpr bool is_tensor(int e) { return e == PRO_TENSOR || e == PRO_TENSOR2; }
@@ -218,6 +222,7 @@ struct EpiRow {
   u32 g;  // PRO_AUTOMORPH (a0, a1 = c0, c1 of the limb; o0 = base or null; ext); combine: e_g
   u32 xg;  // EPI_KSQG / PRO_KSPG: the Galois element ext is gathered through
   u32 e;  // PRO_BFVT: which tensor output (0, 1, 2) this poly is; EPI_KSQT: b
+  u32 jown;  // EPI_KSQT: the digit this limb belongs to (its ext word is d2 R, formed here)
   const u64 *src;  // PRO_CONV: source limb 0 of this poly (limb i at src + i N)
   u64 h[4];        // PRO_CONV: h[i][m] of this workgroup's target limb
   u64 lift_sub;    // PRO_CONV, one source, rescale lift: q_l mod q_m
@@ -601,7 +606,9 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
         const u32 kr = IO::k_reg(st * ST);
 #pragma unroll
         for (int j = 0; j < KD; ++j) {
-          if constexpr (ksq_gather(EPI)) {
+          if (ksq_tensor(EPI) && j == (int)ep.jown) {
+            // EPI_KSQT: the own digit's ext word is formed from a1 b1 (not stored)
+          } else if constexpr (ksq_gather(EPI)) {
 #pragma unroll
             for (int h = 0; h < ST; ++h)
               slot[j][h] = ld_b(ep.kext + j * ep.ext_j, aut_src<LOG_N>((voff >> 3) + kr + h, ep.xg));
@@ -619,8 +626,9 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
           }
         }
       };
-      // EPI_KSQT: the tensor operands of the base, (a0, b0) for b = 0 and
-      // (a0, a1, b0, b1) for b = 1 (TM = 1, 2), loaded in the step that uses them.
+      // EPI_KSQT: the tensor operands (a0, a1, b0, b1) of the base (d0 for b = 0,
+      // d1 for b = 1: TM = 1, 2) and of the own digit's ext word d2 R, loaded in
+      // the step that uses them.
       // A ring of them beside the key-switching one took the pass past 128 VGPRs
       // (one step ahead: no faster, profiles/r05/ab_tensor_split.txt).  The b = 1
       // workgroup follows the b = 0 one on the same XCD (the remap in ntt_pass),
@@ -633,7 +641,6 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
           const u64 *src[4] = {ep.a0, ep.a1, ep.b0, ep.b1};
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            if (TM == 1 && (i & 1)) continue;
             if constexpr (ST == 2) {
               const u64x2 v2 = ld2_b(src[i] + kr, voff);
               slot[i][0] = v2.x, slot[i][1] = v2.y;
@@ -643,6 +650,9 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
           }
         }
       };
+      // EPI_KSQT: R^3 mod q (canonical), the own digit's scale
+      u64 r3 = 0;
+      if constexpr (ksq_tensor(EPI)) r3 = csub(mont_mul<SP>(mi.r2, mi.r2, mi), q);
       const auto store_rows = [&](auto tm) {
         constexpr int TM = decltype(tm)::value;
         if constexpr (is_ksq(EPI)) {
@@ -682,9 +692,14 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
                 // below 1.5q (2q generic), so one subtraction of 4q (WIDE) leaves
                 // the lazy sum below 4q; otherwise it is made canonical.
                 u64 e[KD], k[KD], pr[KD];
+                u64 eown = 0;
+                if constexpr (TM != 0) {
+                  // d2 R = (a1 b1 R^-1) R^3 R^-1, below 1.5q (the product takes it lazy)
+                  eown = mont_mul<SP>(mont_reduce<SP>(mul128(t[1][h], t[3][h]), mi), r3, mi);
+                }
 #pragma unroll
                 for (int j = 0; j < KD; ++j) {
-                  e[j] = ek[st % (PDS + 1)][j][h];
+                  e[j] = TM != 0 && j == (int)ep.jown ? eown : ek[st % (PDS + 1)][j][h];
                   k[j] = ek[st % (PDS + 1)][KD + j][h];
                 }
                 if constexpr (SP) {
@@ -825,21 +840,21 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
           }
           const u64 t = mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi);  // d2 in [0, 2q)
           x[st * ST + h] = csub(t, mi.q);
-          oe[h] = csub(mont_mul<SP>(t, mi.r2, mi), mi.q);  // d2 R
+          if constexpr (ALL) oe[h] = csub(mont_mul<SP>(t, mi.r2, mi), mi.q);  // d2 R
         }
         const u32 kr = GZ::k_reg(st * ST);
         if constexpr (ST == 2) {
           if constexpr (ALL) {
             st2_e(ep.o0 + kr, voff, u64x2{o0[0], o0[1]});
             st2_e(ep.o1 + kr, voff, u64x2{o1[0], o1[1]});
+            st2_e(ep.ext + kr, voff, u64x2{oe[0], oe[1]});
           }
-          st2_e(ep.ext + kr, voff, u64x2{oe[0], oe[1]});
         } else {
           if constexpr (ALL) {
             st_e(ep.o0 + kr, voff, o0[0]);
             st_e(ep.o1 + kr, voff, o1[0]);
+            st_e(ep.ext + kr, voff, oe[0]);
           }
-          st_e(ep.ext + kr, voff, oe[0]);
         }
       }
     } else if constexpr (EPI == PRO_BFVT) {
@@ -1172,7 +1187,7 @@ int launch_persist(fhe_ctx *c, const NttArgs &a, u32 n_jobs) {
 // The tensor prologue asks for 4 waves per SIMD (the LDS allows 4 workgroups
 // per CU anyway), so its 16-byte operand pairs stay within 128 VGPRs
 __host__ __device__ constexpr int pass_min_waves(int EPI, bool SP, int threads) {
-  return threads != 256 ? 1 : (PAIR_IO && (is_tensor(EPI) || ksq_tensor(EPI)) && SP) ? 4 : NTT_MINW;
+  return threads != 256 ? 1 : (PAIR_IO && is_tensor(EPI) && SP) ? 4 : (ksq_tensor(EPI) && SP) ? KSQT_MINW : NTT_MINW;
 }
 template <int LOG_N, int S, int LOGR, int W, bool INV, bool COLS, bool SP, int EPI, int WM>
 __global__ void __launch_bounds__(W << (S - LOGR), pass_min_waves(EPI, SP, W << (S - LOGR)))
@@ -1309,6 +1324,7 @@ __global__ void __launch_bounds__(W << (S - LOGR), pass_min_waves(EPI, SP, W << 
       ep.b0 = a.e_tb + o;
       ep.b1 = ep.b0 + LN;
       ep.e = cpoly & 1;
+      ep.jown = limb / a.t_alpha;
     }
   }
   if constexpr (is_tensor(EPI)) {

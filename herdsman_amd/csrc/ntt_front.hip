@@ -6,7 +6,8 @@
 // CKKS mul+relin front end: the tensor product fused into the first pass of
 // the inverse NTT of d2 (PRO_TENSOR).  a, b, out: [n][2][L][N] (out may alias
 // a or b); dc [n][L][N] receives INTT(d2); ext's own-digit slots receive d2 R.
-// d2_only: out is left alone (PRO_TENSOR2: only a1 and b1 are read).
+// d2_only: out and ext are left alone (PRO_TENSOR2: only a1 and b1 are read;
+// EPI_KSQT forms d0, d1 and the own digit's ext word d2 R).
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig,
                           bool d2_only) {
   const u32 L = c->L, QP = c->L + c->K;

@@ -51,6 +51,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
       if (tsrc) {
         a.e_ta = tsrc->a + (size_t)p0 * L * N;  // poly p0 = 2 ct: ciphertext ct's a_0
         a.e_tb = tsrc->b + (size_t)p0 * L * N;
+        a.t_alpha = c->alpha;  // the own digit of limb i: i / alpha (its ext word is formed, not read)
       }
       a.e_ext_g = ext_g & ((2u << c->log_n) - 1);
       if (rb) {
