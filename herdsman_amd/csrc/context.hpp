@@ -72,6 +72,7 @@ struct fhe_ctx {
   u64 *d_tw_inv = nullptr;     // [nmod][N]  psi^-brv(i) R
   u64 *d_ninv = nullptr;       // [nmod]     N^-1 R
   u64 *d_pinv = nullptr;       // [L]        P^-1 R mod q_i
+  u64 *d_pr2 = nullptr;        // [L]        P R^2 mod q_i (the fused finish folds its base into acc as base P)
   u64 *d_r2 = nullptr;         // [nmod]     R^2 mod q (x -> x R)
   ConvTab *d_modup = nullptr;  // device array [ceil(L/alpha)], h scaled by R^2
   ConvTab moddown{};           // P -> Q, h scaled by R
@@ -194,6 +195,7 @@ struct ConvSrc {
 // ModDown finish is formed from the ciphertexts a, b [n][2][L][N] themselves
 struct TensorSrc {
   const u64 *a, *b;
+  bool fused;  // the whole finish in one kernel (ntt_ks_fused_finish_launch); ModUp skips its Q row passes
 };
 // Hoisted rotations of few ciphertexts: nr Galois elements' gather passes in
 // one launch (poly p of the batch = rotation p / (2 n), ciphertext poly p % (2 n))
@@ -212,7 +214,8 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
 // converted limbs (PRO_CONV; sources = dc's digit limbs, scaled by the INTT
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
 // the lazy (< 8q) NTT outputs times R
-int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j);
+// (q_rows false: the Q targets keep their column-pass outputs, for the fused finish)
+int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows = true);
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n);
 // INTT(acc_P) with the P limbs' key-switching inner product in its first pass
 // (ext_g != 0: ext is read as sigma_g(ext), the hoisted rotation's inner product)
@@ -221,6 +224,12 @@ int ntt_inv_ksp_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32
                        bool all_limbs = false, const RotBatch *rb = nullptr);
 // (base null: sigma(c0) is not stored; the combine then reads it with base_g)
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig);
+// the fused key-switch finish of CKKS mul+relin (ntt_ksf.hip): the row
+// transforms of the non-own ModUp digits' Q limbs and of NTT(conv), the inner
+// product and the ModDown finish in one workgroup per (limb, ct, row block)
+bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig);
+int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, const u64 *ksk, u32 ndig,
+                               const u64 *ta, const u64 *tb, u64 *out, u32 n);
 // d2_only (PRO_TENSOR2, two-pass sizes): out is not written; the ModDown
 // finish forms d0 and d1 (ntt_fwd_combine_launch with a TensorSrc)
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig,

@@ -262,14 +262,16 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p, u32 alpha = 0) {
   // key-switching tables
   if (c->K) {
     const u32 L = c->L, QP = c->L + c->K;
-    std::vector<u64> pinv(L);
+    std::vector<u64> pinv(L), pr2(L);
     for (u32 i = 0; i < L; ++i) {
       const u64 q = c->moduli[i];
       u64 P = 1;
       for (u32 k = 0; k < c->K; ++k) P = hmul(P, c->moduli[L + k] % q, q);
       pinv[i] = tomont(hinv(P, q), q);
+      pr2[i] = tomont(tomont(P, q), q);
     }
     c->d_pinv = (u64 *)ctx_upload(c, pinv.data(), sizeof(u64) * L);
+    c->d_pr2 = (u64 *)ctx_upload(c, pr2.data(), sizeof(u64) * L);
     std::vector<ConvTab> tabs;
     for (u32 j = 0; j * c->alpha < L; ++j) {
       const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
@@ -285,7 +287,7 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p, u32 alpha = 0) {
     for (u32 k = 0; k < c->K; ++k) src.push_back(L + k);
     for (u32 i = 0; i < L; ++i) dst.push_back(i);
     c->moddown = make_conv_tab(c, src, dst, 1, c->fold_ninv);
-    if (!c->d_pinv || !c->d_modup || !c->moddown.h) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
+    if (!c->d_pinv || !c->d_pr2 || !c->d_modup || !c->moddown.h) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
     // ModDown fused into NTT(conv): INTT(acc_P)'s output constants carry the
     // conversion's (P/p_k)^-1 and N^-1 (two-pass sizes, at most 4 sources)
     c->fuse_moddown = c->fold_ninv && c->log_n >= 15 && c->K <= 4;

@@ -1,0 +1,260 @@
+// ntt_ksf.hip -- the fused key-switch finish of CKKS mul+relin (KSF)
+// (kernel templates: ntt_core.hpp)
+//
+// With the tensor product split (PRO_TENSOR2 + EPI_KSQT) one ciphertext's key
+// switch still moves the Q limbs of the non-own ModUp digits through HBM twice
+// more than it must: the ModUp row pass reads their column-pass intermediates
+// and writes ext, and EPI_KSQT reads ext back, once per output poly b.  Here
+// ONE workgroup per (limb, ciphertext, row block) does all of it for both b:
+//   1. the own digit and the base, from the ciphertexts a, b (as EPI_KSQT):
+//        acc_b = (d2 R) ksk_own,b R^-1 + base_b P      (base_0 = a0 b0, base_1 = a0 b1 + a1 b0)
+//   2. every non-own digit j: the row transform of its ModUp intermediate
+//      (the forward row pass, in registers), then acc_b += ext_j ksk_j,b R^-1
+//   3. for b = 0, 1: the row transform of NTT(conv_b)'s intermediate and the
+//      ModDown finish out_b = (acc_b - conv_b) P^-1 = base_b + (acc_b' - conv_b) P^-1
+// so the ModUp row pass runs over the P limbs only (ntt_fwd_modup_launch) and
+// ext's Q limbs are never stored.  The two accumulators (32 words per thread)
+// stay in registers across the four row transforms: 3 waves per SIMD.
+// Bit-exact with the unfused path: the same butterflies (run_group) on the
+// same lazy ranges, every sum reduced mod q_i (acc is canonical before the finish).
+#include "ntt_core.hpp"
+
+#ifndef KSF_FUSE
+#define KSF_FUSE 1  // CKKS mul+relin: the fused key-switch finish where it applies (ks_fused_finish_ok)
+#endif
+#ifndef KSF_LSW
+#define KSF_LSW 4  // butterflies per lock-step chunk (run_group LSW): 8 needs more temporaries than the accumulators leave
+#endif
+#ifndef KSF_MINW
+#define KSF_MINW 3  // minimum waves per SIMD (the accumulators take 64 VGPRs)
+#endif
+
+namespace {
+
+// a loop unrolled by construction: f(integral_constant<int, i>) for i < N (the
+// unroll pragma gives up on these bodies for size, and a rolled loop over the
+// accumulators would put them in scratch)
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F &&f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+struct KsfArgs {
+  const u64 *conv;      // [2n][L][N] NTT(conv)'s column-pass output (ModDown)
+  const u64 *ext;       // [n][ndig][QP][N] ModUp's column-pass outputs (Q limbs of the non-own digits)
+  const u64 *ksk;       // [ndig][2][kQP][N]
+  const u64 *ta, *tb;   // [n][2][L][N] the ciphertexts
+  u64 *out;             // [n][2][L][N]
+  const ModInfo *mods;  // the Q limbs first
+  const u64 *tw;        // forward twiddles [nmod][N]
+  const u64 *pinv;      // [L] P^-1 R
+  const u64 *pr2;       // [L] P R^2
+  u32 L, QP, kQP, ndig, alpha;
+};
+
+template <int LOG_N, int KD, bool WIDE>
+__global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
+  constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
+  using G0 = Grp<S, LOGR, 0>;
+  using G1 = Grp<S, LOGR, 1>;
+  using IO = IoL<S, LOGR>;
+  static_assert(IO::STEP == 2 && (S + LOGR - 1) / LOGR == 2, "two 16-word groups, pair IO");
+  extern __shared__ u64 lds[];
+  constexpr size_t N = (size_t)1 << LOG_N;
+
+  // (row block, ciphertext, limb); as EPI_KSQ, every ciphertext of one (limb,
+  // row block) on consecutive workgroup ids of ONE XCD, so the limb's key rows
+  // stay in that XCD's L2 for the whole batch
+  const u32 tid = threadIdx.x;
+  u32 bx = blockIdx.x, ct = blockIdx.y, limb = blockIdx.z;
+  if (((gridDim.x * gridDim.z) & 7) == 0) {
+    const u32 np = gridDim.y, lin = blockIdx.x + gridDim.x * (blockIdx.y + np * blockIdx.z);
+    const u32 r = lin >> 3, g = (r / np) * 8 + (lin & 7);
+    ct = r % np;
+    bx = g % gridDim.x;
+    limb = g / gridDim.x;
+  }
+  const ModInfo mi = a.mods[limb];
+  const u64 q = mi.q, q2 = 2 * q;
+  const u64 *tw = a.tw + ((size_t)limb << LOG_N);
+  const u32 ts = tid % (1u << (S - LOGR)), w = tid / (1u << (S - LOGR));
+  const u32 row = bx * W + w, gb = row << S;
+  const u32 vin = (gb + G0::k_thr(ts)) << 3;  // the row pass's load layout (group 0)
+  const u32 vio = (gb + IO::k_thr(ts)) << 3;  // the re-laid-out store layout (pairs)
+  const u32 jown = limb / a.alpha;
+  const u64 *kb = a.ksk + (size_t)limb * N;  // key row of digit j, poly b: + j kj + b kbs
+  const size_t kj = (size_t)2 * a.kQP * N, kbs = (size_t)a.kQP * N;
+  const u64 *eb = a.ext + ((size_t)ct * a.ndig * a.QP + limb) * N;  // digit j: + j QP N
+  const size_t LN = (size_t)a.L * N;
+  const size_t co = ((size_t)2 * ct * a.L + limb) * N;  // (ct, poly 0, limb) of [n][2][L][N]
+  const u64 *a0 = a.ta + co, *a1 = a0 + LN, *b0 = a.tb + co, *b1 = b0 + LN;
+
+  u64 nq1 = 0 - q, nq2 = 0 - q2, nq4 = 0 - 2 * q2;
+  asm("" : "+s"(nq1));
+  asm("" : "+s"(nq2));
+  asm("" : "+s"(nq4));
+
+  // the forward row pass of one 16-row block in registers: x in the group-0
+  // layout in, NTT outputs (lazy, as the row pass leaves them) in the IO layout
+  // out.  Each sub-transform's 16 threads sit in one wave, so consecutive
+  // transforms may reuse its LDS slots without a barrier in between.
+  // (scheduling fences around it: left free, the compiler hoists the next
+  // phase's key and operand loads above the transform and spills)
+  const auto row_io = [&](u64 (&x)[R]) {
+    __builtin_amdgcn_sched_barrier(0);
+    u64 t[16];
+    G0::template load_tw<S0>(t, tw, row, ts);
+    run_group<S, LOGR, 0, S0, false, true, WIDE, KSF_LSW>(x, t, q2, mi);
+    G1::template load_tw<S0>(t, tw, row, ts);
+    const u32 l0 = lds_idx<S>(w, G0::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[l0 + G0::k_reg(r) + lds_pad(G0::k_reg(r))] = x[r];
+    __syncthreads();
+    const u32 l1 = lds_idx<S>(w, G1::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))];
+    run_group<S, LOGR, 1, S0, false, true, WIDE, KSF_LSW>(x, t, q2, mi);
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))] = x[r];
+    __syncthreads();
+    const u32 l2 = lds_idx<S>(w, IO::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lds[l2 + IO::k_reg(r) + lds_pad(IO::k_reg(r))];
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // 1. the own digit (d2 R from a1 b1) and the base times P, canonical sums below 2q
+  u64 acc0[R], acc1[R];
+  {
+    const u64 r3 = csub(mont_mul<true>(mi.r2, mi.r2, mi), q);  // R^3
+    const u64 pr2 = a.pr2[limb];
+    const u64 *k0 = kb + jown * kj, *k1 = k0 + kbs;
+    sfor<R / 2>([&](auto I) {
+      constexpr int r = 2 * decltype(I)::value;
+      const u32 kr = IO::k_reg(r);
+      const u64x2 A0 = ld2_b(a0 + kr, vio), A1 = ld2_b(a1 + kr, vio);
+      const u64x2 B0 = ld2_b(b0 + kr, vio), B1 = ld2_b(b1 + kr, vio);
+      const u64x2 K0 = ld2_b(k0 + kr, vio), K1 = ld2_b(k1 + kr, vio);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const u64 x0 = A0[h], x1 = A1[h], y0 = B0[h], y1 = B1[h];
+        const u64 e = mont_mul<true>(mont_reduce<true>(mul128(x1, y1), mi), r3, mi);        // d2 R, < 1.5q
+        const u64 d0p = mont_mul<true>(mont_reduce<true>(mul128(x0, y0), mi), pr2, mi);    // base_0 P
+        U128 t1 = mul128(x0, y1);
+        mac128(t1, x1, y0);
+        const u64 d1p = mont_mul<true>(mont_reduce<true>(t1, mi), pr2, mi);                // base_1 P
+        acc0[r + h] = harvey_csub(mont_mul<true>(e, K0[h], mi) + d0p, nq2);
+        acc1[r + h] = harvey_csub(mont_mul<true>(e, K1[h], mi) + d1p, nq2);
+      }
+    });
+  }
+  // 2. the non-own digits: their ModUp row transform here, then the products
+  for (int j = 0; j < KD; ++j) {
+    if (j == (int)jown) continue;  // uniform
+    u64 x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = ld_d(eb + (size_t)j * a.QP * N + G0::k_reg(r), vin);
+    row_io(x);  // ext_j R, lazy (< 8q WIDE, < 4q)
+    const u64 *k0 = kb + j * kj, *k1 = k0 + kbs;
+    sfor<R / 2>([&](auto I) {
+      constexpr int r = 2 * decltype(I)::value;
+      const u32 kr = IO::k_reg(r);
+      const u64x2 K0 = ld2_b(k0 + kr, vio), K1 = ld2_b(k1 + kr, vio);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acc0[r + h] = harvey_csub(acc0[r + h] + mont_mul<true>(x[r + h], K0[h], mi), nq2);
+        acc1[r + h] = harvey_csub(acc1[r + h] + mont_mul<true>(x[r + h], K1[h], mi), nq2);
+      }
+    });
+  }
+  // 3. NTT(conv_b)'s row transform and the ModDown finish, b = 0, 1
+  u64 cb1 = (WIDE ? 2 * q2 : q2) + 1;  // B q + 1: (acc + cb1) + ~v = acc + B q - v
+  asm("" : "+s"(cb1));
+  const u64 pinv = a.pinv[limb];
+  const auto finish = [&](const u64(&acc)[R], int b) {
+    u64 x[R];
+    const u64 *cv = a.conv + co + b * LN;
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = ld_d(cv + G0::k_reg(r), vin);
+    row_io(x);
+    u64 *ob = a.out + co + b * LN;
+    sfor<R / 2>([&](auto I) {
+      constexpr int r = 2 * decltype(I)::value;
+      u64 o[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const u64 v = harvey_csub(x[r + h], WIDE ? nq4 : nq2);  // below 4q (WIDE) / 2q
+        const u64 s = harvey_csub(acc[r + h], nq1);
+        o[h] = harvey_csub(mont_mul<true>((s + cb1) + ~v, pinv, mi), nq1);
+      }
+      st2_e(ob + IO::k_reg(r), vio, u64x2{o[0], o[1]});
+    });
+  };
+  finish(acc0, 0);
+  finish(acc1, 1);
+}
+
+template <int LOG_N, int KD, bool WIDE>
+int ksf_launch(fhe_ctx *c, const KsfArgs &a, u32 n) {
+  constexpr size_t lds = lds_bytes<8, 16>();
+  const dim3 grid((1u << (LOG_N - 8)) / 16, n, a.L);
+  hipLaunchKernelGGL((ksf_pass<LOG_N, KD, WIDE>), grid, dim3(256), lds, c->stream, a);
+  return fhe_check(c, hipGetLastError(), "ksf_pass launch");
+}
+
+template <int LOG_N, int KD>
+int ksf_dispatch(fhe_ctx *c, const KsfArgs &a, u32 n) {
+  return c->moduli[0] < (1ull << 60) ? ksf_launch<LOG_N, KD, true>(c, a, n) : ksf_launch<LOG_N, KD, false>(c, a, n);
+}
+
+}  // namespace
+
+// The fused finish applies: special moduli, N = 2^15 or 2^16 (a 256-point row
+// pass), at most 3 digits, and the Q limbs in one lazy-schedule class.
+bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig) {
+  if (!KSF_FUSE || !c->special || (c->log_n != 15 && c->log_n != 16) || ndig < 1 || ndig > 3 || !c->L) return false;
+  const bool wide = c->moduli[0] < (1ull << 60);
+  for (u32 i = 1; i < c->L; ++i)
+    if ((c->moduli[i] < (1ull << 60)) != wide) return false;
+  return true;
+}
+
+int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, const u64 *ksk, u32 ndig,
+                               const u64 *ta, const u64 *tb, u64 *out, u32 n) {
+  if (!ks_fused_finish_ok(c, ndig)) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch finish: shape");
+  const size_t N = c->n, L = c->L, QP = c->L + c->K;
+  const u32 per = 65535u;  // gridDim.y
+  for (u32 c0 = 0; c0 < n; c0 += per) {
+    const u32 nc = std::min(per, n - c0);
+    KsfArgs a{};
+    a.conv = conv + (size_t)c0 * 2 * L * N;
+    a.ext = ext + (size_t)c0 * ndig * QP * N;
+    a.ksk = ksk;
+    a.ta = ta + (size_t)c0 * 2 * L * N;
+    a.tb = tb + (size_t)c0 * 2 * L * N;
+    a.out = out + (size_t)c0 * 2 * L * N;
+    a.mods = c->d_mods;
+    a.tw = c->d_tw_fwd;
+    a.pinv = c->d_pinv;
+    a.pr2 = c->d_pr2;
+    a.L = c->L;
+    a.QP = (u32)QP;
+    a.kQP = ctx_key_qp(c);
+    a.ndig = ndig;
+    a.alpha = c->alpha;
+    int rc;
+    if (c->log_n == 15) {
+      rc = ndig == 1 ? ksf_dispatch<15, 1>(c, a, nc) : ndig == 2 ? ksf_dispatch<15, 2>(c, a, nc)
+                                                                  : ksf_dispatch<15, 3>(c, a, nc);
+    } else {
+      rc = ndig == 1 ? ksf_dispatch<16, 1>(c, a, nc) : ndig == 2 ? ksf_dispatch<16, 2>(c, a, nc)
+                                                                  : ksf_dispatch<16, 3>(c, a, nc);
+    }
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}

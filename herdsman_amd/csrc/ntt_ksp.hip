@@ -9,7 +9,7 @@
 // INTT through d_iscale) as its prologue (PRO_CONV), so the converted limbs
 // never make an HBM round trip; the row pass leaves lazy outputs (< 8q) for
 // the inner product on special moduli, as keyswitch_run's separate NTT does.
-int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j) {
+int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows) {
   const u32 L = c->L, QP = c->L + c->K, N = c->n;
   const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
   const ConvTab &tab = c->modup_tabs[j];
@@ -41,7 +41,11 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
     ap.c_h = tab.h + (L - (hi - lo));
     const int wq = wide_mode(c, aq.map), wp = wide_mode(c, ap.map);
     int rc;
-    if (wq != 2 && wp != 2 && wq != wp && aq.map.cnt && ap.map.cnt) {
+    if (!q_rows) {
+      // the fused finish transforms the Q targets' rows itself (ntt_ksf.hip)
+      if ((rc = ntt_conv_col(c, a, n_jobs))) return rc;
+      rc = ap.map.cnt ? ntt_row_plain(c, ap, false, np * ap.map.cnt) : FHE_OK;
+    } else if (wq != 2 && wp != 2 && wq != wp && aq.map.cnt && ap.map.cnt) {
 #if MODUP_COL_SPLIT
       if ((rc = ntt_conv_col(c, aq, np * aq.map.cnt))) return rc;
       if ((rc = ntt_conv_col(c, ap, np * ap.map.cnt))) return rc;

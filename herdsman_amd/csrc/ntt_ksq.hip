@@ -90,6 +90,13 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
         rc = ntt_col_plain(c, a, false, n_jobs);
       }
       if (rc) return rc;
+      if (tsrc && tsrc->fused) {
+        // the row transforms of ext's Q limbs and of NTT(conv), the inner
+        // product and the finish in one kernel (ntt_ksf.hip)
+        rc = ntt_ks_fused_finish_launch(c, a.map.base, a.e_ext, ksk, ndig, a.e_ta, a.e_tb, a.e_out, np / 2);
+        if (rc) return rc;
+        continue;
+      }
       switch (ext ? ndig + (ext_g || rb ? 4 : 0) + (tsrc ? 8 : 0) : 0) {
         case 9: rc = row_pass<EPI_KSQT>(c, a, false, n_jobs); break;
         case 10: rc = row_pass<EPI_KSQT + 1>(c, a, false, n_jobs); break;

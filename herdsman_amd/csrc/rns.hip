@@ -979,7 +979,7 @@ static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
 // Split in two for hoisted rotations: ks_extend (steps 1-3: INTT, ModUp, NTT of
 // the converted limbs, into w.ext) runs once per input, ks_finish (steps 4-6:
 // inner product, ModDown) once per key.
-static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is_coef) {
+static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is_coef, bool q_rows = true) {
   const u32 L = c->L, QP = L + c->K, N = c->n, ndig = w.ndig;
   u64 *dc = w.dc, *ext = w.ext;
   int rc;
@@ -994,8 +994,9 @@ static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is
   if (fused_modup) {
     // 2-3. ModUp + NTT of the converted limbs, one digit at a time
     for (u32 j = 0; j < ndig; ++j)
-      if ((rc = ntt_fwd_modup_launch(c, dc, ext, n, ndig, j))) return rc;
+      if ((rc = ntt_fwd_modup_launch(c, dc, ext, n, ndig, j, q_rows))) return rc;
   }
+  if (!q_rows && !fused_modup) return fhe_fail(c, FHE_ERR_INVALID, "ModUp without Q rows: fused ModUp only");
   // 2. ModUp: every non-own limb of every digit
   if (!fused_modup && (rc = SP_DISPATCH(c, modup_impl, c, dc, L, ext, n, ndig))) return rc;
   // 3. NTT the converted limbs (all limbs for BFV, whose own limbs are coefficient form)
@@ -1056,7 +1057,7 @@ static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, 
 
 static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
                          bool ntt_form, bool dc_is_coef = false, u32 base_g = 0, const TensorSrc *tsrc = nullptr) {
-  int rc = ks_extend(c, w, n, ntt_form, dc_is_coef);
+  int rc = ks_extend(c, w, n, ntt_form, dc_is_coef, !(tsrc && tsrc->fused));
   return rc ? rc : ks_finish(c, w, w.ext, ksk, base, out, n, add_mask, ntt_form, base_g, 0, tsrc);
 }
 
@@ -1150,10 +1151,11 @@ int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, 
   if (rc) return rc;
   const KsWs w = ks_layout(c, n, (u64 *)ws);
   const size_t bytes = sizeof(u64) * 2 * c->L * c->n * (size_t)n;
-  const bool split = TENSOR_SPLIT && c->log_n > 14 && c->fuse_moddown && w.ndig <= 3 && KSP_FUSE &&
+  // (special moduli: the generic-product EPI_KSQT keeps its operand ring in scratch, -18%)
+  const bool split = TENSOR_SPLIT && c->special && c->log_n > 14 && c->fuse_moddown && w.ndig <= 3 && KSP_FUSE &&
                      !ranges_overlap(out, a, bytes) && !ranges_overlap(out, b, bytes);
   if ((rc = ntt_inv_tensor_launch(c, a, b, out, w.dc, w.ext, n, w.ndig, split))) return rc;
-  const TensorSrc ts{a, b};
+  const TensorSrc ts{a, b, split && c->fuse_modup && ks_fused_finish_ok(c, w.ndig)};
   return keyswitch_run(c, w, rlk, out, out, n, 3u, true, true, 0, split ? &ts : nullptr);
 }
 
