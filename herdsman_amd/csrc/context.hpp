@@ -196,6 +196,7 @@ struct ConvSrc {
 struct TensorSrc {
   const u64 *a, *b;
   bool fused;  // the whole finish in one kernel (ntt_ks_fused_finish_launch); ModUp skips its Q row passes
+  u32 g = 0;   // fused only: a CKKS rotation by g instead (a = the ciphertexts, read through sigma_g; b unused)
 };
 // Hoisted rotations of few ciphertexts: nr Galois elements' gather passes in
 // one launch (poly p of the batch = rotation p / (2 n), ciphertext poly p % (2 n))
@@ -228,8 +229,9 @@ int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *d
 // transforms of the non-own ModUp digits' Q limbs and of NTT(conv), the inner
 // product and the ModDown finish in one workgroup per (limb, ct, row block)
 bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig);
+// (g != 0: the rotation's finish, ta = the ciphertexts read through sigma_g, tb unused)
 int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, const u64 *ksk, u32 ndig,
-                               const u64 *ta, const u64 *tb, u64 *out, u32 n);
+                               const u64 *ta, const u64 *tb, u64 *out, u32 n, u32 g = 0);
 // d2_only (PRO_TENSOR2, two-pass sizes): out is not written; the ModDown
 // finish forms d0 and d1 (ntt_fwd_combine_launch with a TensorSrc)
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig,

@@ -911,7 +911,7 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
         const u64 y0 = y[r % (PD + 1)][0], y1 = y[r % (PD + 1)][1];
         if (ep.o0) st_e(ep.o0 + kr, voff, y0);
         x[r] = y1;
-        st_e(ep.ext + kr, voff, csub63(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
+        if (ep.ext) st_e(ep.ext + kr, voff, csub63(mont_mul<SP>(y1, mi.r2, mi), mi.q));  // sigma(c1) R
       }
     } else if constexpr (is_ksp(EPI)) {
       // acc_P = sum_j ext_j ksk_j R^-1 (ks_inner_kernel; ext carries R) at the
@@ -1355,7 +1355,7 @@ __global__ void __launch_bounds__(W << (S - LOGR), pass_min_waves(EPI, SP, W << 
     ep.a0 = a.t_a + o;
     ep.a1 = ep.a0 + LN;
     ep.o0 = a.t_out ? a.t_out + o : nullptr;
-    ep.ext = a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N);
+    ep.ext = a.t_ext ? a.t_ext + (((size_t)(poly * a.t_ndig + limb / a.t_alpha) * a.t_QP + limb) << LOG_N) : nullptr;
     ep.g = a.t_g;
   }
   if constexpr (is_conv(EPI)) {

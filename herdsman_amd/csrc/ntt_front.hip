@@ -51,7 +51,8 @@ int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 
 // CKKS rotation front end: the NTT-domain automorphism sigma_g (and the KS
 // preparation of sigma_g(c1)) fused into the first pass of its inverse NTT
 // (PRO_AUTOMORPH).  ct [n][2][L][N] must not alias base; base[ct][0] receives
-// sigma_g(c0), dc INTT(sigma_g(c1)), ext's own-digit slots sigma_g(c1) R.
+// sigma_g(c0), dc INTT(sigma_g(c1)), ext's own-digit slots sigma_g(c1) R (ext
+// null: not stored, the fused key-switch finish forms them).
 int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *dc, u64 *ext, u32 n, u32 ndig) {
   const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
@@ -67,7 +68,7 @@ int ntt_inv_automorph_launch(fhe_ctx *c, const u64 *ct, u32 g, u64 *base, u64 *d
     t.log_n = c->log_n;
     t.t_a = ct + (size_t)p0 * 2 * L * N;
     t.t_out = base ? base + (size_t)p0 * 2 * L * N : nullptr;
-    t.t_ext = ext + (size_t)p0 * ndig * QP * N;
+    t.t_ext = ext ? ext + (size_t)p0 * ndig * QP * N : nullptr;
     t.t_L = L;
     t.t_QP = QP;
     t.t_alpha = c->alpha;

@@ -1,4 +1,4 @@
-// ntt_ksf.hip -- the fused key-switch finish of CKKS mul+relin (KSF)
+// ntt_ksf.hip -- the fused key-switch finish of CKKS mul+relin and rotation (KSF)
 // (kernel templates: ntt_core.hpp)
 //
 // With the tensor product split (PRO_TENSOR2 + EPI_KSQT) one ciphertext's key
@@ -15,6 +15,9 @@
 // so the ModUp row pass runs over the P limbs only (ntt_fwd_modup_launch) and
 // ext's Q limbs are never stored.  The two accumulators (32 words per thread)
 // stay in registers across the four row transforms: 3 waves per SIMD.
+// A rotation (ROT) runs the same finish with the own digit's word sigma_g(c1) R
+// and the base sigma_g(c0) (poly 0) gathered from the ciphertext, so
+// PRO_AUTOMORPH stores neither.
 // Bit-exact with the unfused path: the same butterflies (run_group) on the
 // same lazy ranges, every sum reduced mod q_i (acc is canonical before the finish).
 #include "ntt_core.hpp"
@@ -54,9 +57,12 @@ struct KsfArgs {
   const u64 *pinv;      // [L] P^-1 R
   const u64 *pr2;       // [L] P R^2
   u32 L, QP, kQP, ndig, alpha;
+  u32 g;                // ROT: the Galois element (ta = the ciphertexts, read through sigma_g)
 };
 
-template <int LOG_N, int KD, bool WIDE>
+// ROT: a CKKS rotation's finish instead: the own digit's word is sigma_g(c1) R
+// and the base sigma_g(c0) (poly 0 only), both gathered from the ciphertext
+template <int LOG_N, int KD, bool WIDE, bool ROT>
 __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
   constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
   using G0 = Grp<S, LOGR, 0>;
@@ -129,7 +135,23 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
 
   // 1. the own digit (d2 R from a1 b1) and the base times P, canonical sums below 2q
   u64 acc0[R], acc1[R];
-  {
+  if constexpr (ROT) {
+    const u64 pr = csub(mont_mul<true>(a.pr2[limb], 1, mi), q);  // P R
+    const u64 *k0 = kb + jown * kj, *k1 = k0 + kbs;
+    sfor<R / 2>([&](auto I) {
+      constexpr int r = 2 * decltype(I)::value;
+      const u32 kr = IO::k_reg(r);
+      const u64x2 K0 = ld2_b(k0 + kr, vio), K1 = ld2_b(k1 + kr, vio);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const u32 src = aut_src<LOG_N>((vio >> 3) + kr + h, a.g);
+        const u64 y0 = ld_b(a0, src), y1 = ld_b(a1, src);  // sigma_g(c0), sigma_g(c1)
+        const u64 e = mont_mul<true>(y1, mi.r2, mi);        // sigma_g(c1) R, < 1.5q
+        acc0[r + h] = harvey_csub(mont_mul<true>(e, K0[h], mi) + mont_mul<true>(y0, pr, mi), nq2);
+        acc1[r + h] = mont_mul<true>(e, K1[h], mi);
+      }
+    });
+  } else {
     const u64 r3 = csub(mont_mul<true>(mi.r2, mi.r2, mi), q);  // R^3
     const u64 pr2 = a.pr2[limb];
     const u64 *k0 = kb + jown * kj, *k1 = k0 + kbs;
@@ -198,17 +220,19 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
   finish(acc1, 1);
 }
 
-template <int LOG_N, int KD, bool WIDE>
+template <int LOG_N, int KD, bool WIDE, bool ROT>
 int ksf_launch(fhe_ctx *c, const KsfArgs &a, u32 n) {
   constexpr size_t lds = lds_bytes<8, 16>();
   const dim3 grid((1u << (LOG_N - 8)) / 16, n, a.L);
-  hipLaunchKernelGGL((ksf_pass<LOG_N, KD, WIDE>), grid, dim3(256), lds, c->stream, a);
+  hipLaunchKernelGGL((ksf_pass<LOG_N, KD, WIDE, ROT>), grid, dim3(256), lds, c->stream, a);
   return fhe_check(c, hipGetLastError(), "ksf_pass launch");
 }
 
 template <int LOG_N, int KD>
 int ksf_dispatch(fhe_ctx *c, const KsfArgs &a, u32 n) {
-  return c->moduli[0] < (1ull << 60) ? ksf_launch<LOG_N, KD, true>(c, a, n) : ksf_launch<LOG_N, KD, false>(c, a, n);
+  const bool wide = c->moduli[0] < (1ull << 60);
+  if (a.g) return wide ? ksf_launch<LOG_N, KD, true, true>(c, a, n) : ksf_launch<LOG_N, KD, false, true>(c, a, n);
+  return wide ? ksf_launch<LOG_N, KD, true, false>(c, a, n) : ksf_launch<LOG_N, KD, false, false>(c, a, n);
 }
 
 }  // namespace
@@ -224,7 +248,7 @@ bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig) {
 }
 
 int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, const u64 *ksk, u32 ndig,
-                               const u64 *ta, const u64 *tb, u64 *out, u32 n) {
+                               const u64 *ta, const u64 *tb, u64 *out, u32 n, u32 g) {
   if (!ks_fused_finish_ok(c, ndig)) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch finish: shape");
   const size_t N = c->n, L = c->L, QP = c->L + c->K;
   const u32 per = 65535u;  // gridDim.y
@@ -235,7 +259,8 @@ int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, cons
     a.ext = ext + (size_t)c0 * ndig * QP * N;
     a.ksk = ksk;
     a.ta = ta + (size_t)c0 * 2 * L * N;
-    a.tb = tb + (size_t)c0 * 2 * L * N;
+    a.tb = g ? nullptr : tb + (size_t)c0 * 2 * L * N;
+    a.g = g;
     a.out = out + (size_t)c0 * 2 * L * N;
     a.mods = c->d_mods;
     a.tw = c->d_tw_fwd;

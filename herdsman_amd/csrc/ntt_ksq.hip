@@ -19,9 +19,12 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
     return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch inner product: log_n / digits");
   if (base_g && c->log_n <= 14) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated combine base: log_n");
   if ((ext_g || rb) && !ext) return fhe_fail(c, FHE_ERR_INVALID, "gathered ext without the fused inner product");
-  // tsrc: the base is formed from the ciphertexts (EPI_KSQT), added to both polys
-  if (tsrc && (!ext || ext_g || rb || base_g || add_mask != 3u))
-    return fhe_fail(c, FHE_ERR_INVALID, "split tensor product: plain fused inner product only");
+  // tsrc: the base is formed from the ciphertexts (EPI_KSQT), added to both polys;
+  // tsrc->g: a rotation's fused finish (base sigma_g(c0) on poly 0)
+  if (tsrc && (!ext || ext_g || rb ||
+               (tsrc->g ? !tsrc->fused || (base_g & ((2u << c->log_n) - 1)) != tsrc->g || add_mask != 1u
+                                                : base_g || add_mask != 3u)))
+    return fhe_fail(c, FHE_ERR_INVALID, "fused finish: plain fused inner product only");
   // rb: the n_polys = 2 n nr polys of rb->nr rotations in one chunk; base (the
   // ciphertexts, read through each rotation's sigma_g) has 2 n polys
   if (rb && (rb->nr < 1 || rb->nr > FHE_ROT_BATCH || n_polys > COMBINE_CHUNK || n_polys % (2 * rb->nr)))
@@ -50,7 +53,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
       a.e_kQP = ctx_key_qp(c);
       if (tsrc) {
         a.e_ta = tsrc->a + (size_t)p0 * L * N;  // poly p0 = 2 ct: ciphertext ct's a_0
-        a.e_tb = tsrc->b + (size_t)p0 * L * N;
+        a.e_tb = tsrc->b ? tsrc->b + (size_t)p0 * L * N : nullptr;
         a.t_alpha = c->alpha;  // the own digit of limb i: i / alpha (its ext word is formed, not read)
       }
       a.e_ext_g = ext_g & ((2u << c->log_n) - 1);
@@ -93,7 +96,8 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
       if (tsrc && tsrc->fused) {
         // the row transforms of ext's Q limbs and of NTT(conv), the inner
         // product and the finish in one kernel (ntt_ksf.hip)
-        rc = ntt_ks_fused_finish_launch(c, a.map.base, a.e_ext, ksk, ndig, a.e_ta, a.e_tb, a.e_out, np / 2);
+        rc = ntt_ks_fused_finish_launch(c, a.map.base, a.e_ext, ksk, ndig, a.e_ta, a.e_tb, a.e_out, np / 2,
+                                        tsrc->g);
         if (rc) return rc;
         continue;
       }

@@ -952,6 +952,9 @@ struct KsWs {
 #ifndef KSP_FUSE
 #define KSP_FUSE 1  // the P limbs' inner product inside INTT(acc_P)'s first pass (0: ks_inner_kernel)
 #endif
+#ifndef ROT_FUSE
+#define ROT_FUSE 1  // CKKS rotation: the fused key-switch finish (ntt_ksf.hip) where it applies
+#endif
 #ifndef TENSOR_SPLIT
 #define TENSOR_SPLIT 1  // CKKS mul+relin: d0, d1 formed in the ModDown finish (ckks_mul_relin_impl)
 #endif
@@ -1174,8 +1177,14 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
     const u64 *ce = ct + (size_t)n * 2 * LN;
     const bool apart = out + (size_t)n * 2 * LN <= ct || ce <= out;
     const bool read_sigma = c->fuse_moddown && apart;
-    if ((rc = ntt_inv_automorph_launch(c, ct, g, read_sigma ? nullptr : base, w.dc, w.ext, n, w.ndig))) return rc;
-    return keyswitch_run(c, w, gk, read_sigma ? ct : base, out, n, 1u, true, true, read_sigma ? g : 0u);
+    // the fused finish (ntt_ksf.hip) forms the own digit's sigma_g(c1) R itself
+    const bool fused = read_sigma && ROT_FUSE && c->fuse_modup && KSP_FUSE && ks_fused_finish_ok(c, w.ndig);
+    if ((rc = ntt_inv_automorph_launch(c, ct, g, read_sigma ? nullptr : base, w.dc, fused ? nullptr : w.ext, n,
+                                       w.ndig)))
+      return rc;
+    const TensorSrc ts{ct, nullptr, true, g & ((2u << c->log_n) - 1)};
+    return keyswitch_run(c, w, gk, read_sigma ? ct : base, out, n, 1u, true, true, read_sigma ? g : 0u,
+                         fused ? &ts : nullptr);
   }
   if (!ntt_form && bfv_fused(c)) {
     // BFV at two-pass sizes: the fused key switch; with out apart from ct,
