@@ -12,8 +12,8 @@
 //      (the forward row pass, in registers), then acc_b += ext_j ksk_j,b R^-1
 //   3. for b = 0, 1: the row transform of NTT(conv_b)'s intermediate and the
 //      ModDown finish out_b = (acc_b - conv_b) P^-1 = base_b + (acc_b' - conv_b) P^-1
-// so the ModUp row pass runs over the P limbs only (ntt_fwd_modup_launch) and
-// ext's Q limbs are never stored.  The two accumulators (32 words per thread)
+// so ext's Q limbs are never stored (the P limbs: ksp_fused_pass below; with
+// both, ntt_fwd_modup_launch runs ModUp's column passes only).  The two accumulators (32 words per thread)
 // stay in registers across the four row transforms: 3 waves per SIMD.
 // A rotation (ROT) runs the same finish with the own digit's word sigma_g(c1) R
 // and the base sigma_g(c0) (poly 0) gathered from the ciphertext, so
@@ -27,6 +27,9 @@
 #endif
 #ifndef KSF_LSW
 #define KSF_LSW 4  // butterflies per lock-step chunk (run_group LSW): 8 needs more temporaries than the accumulators leave
+#endif
+#ifndef KSP_LSW
+#define KSP_LSW 2  // the same for the P side (ksp_fused_pass: 4 spills 11 VGPRs)
 #endif
 #ifndef KSF_MINW
 #define KSF_MINW 3  // minimum waves per SIMD (the accumulators take 64 VGPRs)
@@ -45,6 +48,15 @@ template <int N, class F>
 __device__ __forceinline__ void sfor(F &&f) {
   sfor_impl(f, std::make_integer_sequence<int, N>{});
 }
+
+struct KspArgs {
+  u64 *acc;             // [2n][QP][N]: the P rows receive INTT(acc_P)'s row pass
+  const u64 *ext;       // [n][ndig][QP][N] ModUp's column-pass outputs (P limbs)
+  const u64 *ksk;       // [ndig][2][kQP][N]
+  const ModInfo *mods;
+  const u64 *twf, *twi; // forward / inverse twiddles [nmod][N]
+  u32 L, QP, kQP, kshift, ndig;
+};
 
 struct KsfArgs {
   const u64 *conv;      // [2n][L][N] NTT(conv)'s column-pass output (ModDown)
@@ -235,7 +247,130 @@ int ksf_dispatch(fhe_ctx *c, const KsfArgs &a, u32 n) {
   return wide ? ksf_launch<LOG_N, KD, true, false>(c, a, n) : ksf_launch<LOG_N, KD, false, false>(c, a, n);
 }
 
+// The P side of the same key switch (KSP fused): one workgroup per (P limb,
+// ct, row block) row-transforms every digit's ModUp intermediate of the limb
+// (they are all non-own), forms acc_P,b = sum_j ext_j ksk_j,b R^-1 for b = 0, 1
+// and runs the first (row) pass of INTT(acc_P,b) on it, so the ModUp row pass
+// and PRO_KSP's ext reads go away; the INTT's column pass follows as before.
+template <int LOG_N, int KD, bool WIDE>
+__global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
+  constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
+  using G0 = Grp<S, LOGR, 0>;
+  using G1 = Grp<S, LOGR, 1>;
+  using IO = IoL<S, LOGR>;
+  extern __shared__ u64 lds[];
+  constexpr size_t N = (size_t)1 << LOG_N;
+  const u32 tid = threadIdx.x;
+  u32 bx = blockIdx.x, ct = blockIdx.y, pl = blockIdx.z;  // pl: P limb (0..K-1)
+  if (((gridDim.x * gridDim.z) & 7) == 0) {
+    const u32 np = gridDim.y, lin = blockIdx.x + gridDim.x * (blockIdx.y + np * blockIdx.z);
+    const u32 r = lin >> 3, g = (r / np) * 8 + (lin & 7);
+    ct = r % np;
+    bx = g % gridDim.x;
+    pl = g / gridDim.x;
+  }
+  const u32 limb = a.L + pl;  // index in Q u P
+  const ModInfo mi = a.mods[limb];
+  const u64 q = mi.q, q2 = 2 * q;
+  const u64 *twf = a.twf + ((size_t)limb << LOG_N), *twi = a.twi + ((size_t)limb << LOG_N);
+  const u32 ts = tid % (1u << (S - LOGR)), w = tid / (1u << (S - LOGR));
+  const u32 row = bx * W + w, gb = row << S;
+  const u32 vin = (gb + G0::k_thr(ts)) << 3;
+  const u32 vio = (gb + IO::k_thr(ts)) << 3;
+  const u64 *kb = a.ksk + (size_t)(limb + a.kshift) * N;  // P limbs: key row i + kshift
+  const size_t kj = (size_t)2 * a.kQP * N, kbs = (size_t)a.kQP * N;
+  const u64 *eb = a.ext + ((size_t)ct * a.ndig * a.QP + limb) * N;
+  u64 nq1 = 0 - q, nq2 = 0 - q2;
+  asm("" : "+s"(nq1));
+  asm("" : "+s"(nq2));
+  const auto row_io = [&](u64 (&x)[R]) {
+    __builtin_amdgcn_sched_barrier(0);
+    u64 t[16];
+    G0::template load_tw<S0>(t, twf, row, ts);
+    run_group<S, LOGR, 0, S0, false, true, WIDE, KSP_LSW>(x, t, q2, mi);
+    G1::template load_tw<S0>(t, twf, row, ts);
+    const u32 l0 = lds_idx<S>(w, G0::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[l0 + G0::k_reg(r) + lds_pad(G0::k_reg(r))] = x[r];
+    __syncthreads();
+    const u32 l1 = lds_idx<S>(w, G1::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))];
+    run_group<S, LOGR, 1, S0, false, true, WIDE, KSP_LSW>(x, t, q2, mi);
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))] = x[r];
+    __syncthreads();
+    const u32 l2 = lds_idx<S>(w, IO::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lds[l2 + IO::k_reg(r) + lds_pad(IO::k_reg(r))];
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // acc_P,b over every digit, kept below 2q (the products are below 1.5q)
+  u64 acc0[R], acc1[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc0[r] = acc1[r] = 0;
+  for (int j = 0; j < KD; ++j) {
+    __builtin_amdgcn_sched_barrier(0);  // the next digit's loads stay below this digit's products
+    u64 x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = ld_d(eb + (size_t)j * a.QP * N + G0::k_reg(r), vin);
+    row_io(x);
+    const u64 *k0 = kb + j * kj, *k1 = k0 + kbs;
+    sfor<R / 2>([&](auto I) {
+      constexpr int r = 2 * decltype(I)::value;
+      const u32 kr = IO::k_reg(r);
+      const u64x2 K0 = ld2_b(k0 + kr, vio), K1 = ld2_b(k1 + kr, vio);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acc0[r + h] = harvey_csub(acc0[r + h] + mont_mul<true>(x[r + h], K0[h], mi), nq2);
+        acc1[r + h] = harvey_csub(acc1[r + h] + mont_mul<true>(x[r + h], K1[h], mi), nq2);
+      }
+    });
+  }
+  // the first (row) pass of INTT(acc_P,b): canonical acc in the IO layout ->
+  // group 1 -> group 0, stored in the group-0 layout (as PRO_KSP's pass does)
+  const u32 vst = (gb + G0::k_thr(ts)) << 3;
+  const auto inv_row = [&](const u64(&acc)[R], int b) {
+    __builtin_amdgcn_sched_barrier(0);
+    u64 x[R], t[16];
+    G1::template load_tw<S0>(t, twi, row, ts);
+    const u32 l2 = lds_idx<S>(w, IO::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[l2 + IO::k_reg(r) + lds_pad(IO::k_reg(r))] = harvey_csub(acc[r], nq1);
+    __syncthreads();
+    const u32 l1 = lds_idx<S>(w, G1::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))];
+    run_group<S, LOGR, 1, S0, true, true, false, KSP_LSW>(x, t, q2, mi);
+    G0::template load_tw<S0>(t, twi, row, ts);
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))] = x[r];
+    __syncthreads();
+    const u32 l0 = lds_idx<S>(w, G0::k_thr(ts));
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lds[l0 + G0::k_reg(r) + lds_pad(G0::k_reg(r))];
+    run_group<S, LOGR, 0, S0, true, true, false, KSP_LSW>(x, t, q2, mi);
+    u64 *dst = a.acc + ((size_t)(2 * ct + b) * a.QP + limb) * N;
+#pragma unroll
+    for (int r = 0; r < R; ++r) st_d(dst + G0::k_reg(r), vst, x[r]);
+  };
+  inv_row(acc0, 0);
+  inv_row(acc1, 1);
+}
+
 }  // namespace
+
+template <int LOG_N, int KD, bool WIDE>
+int ksp_launch(fhe_ctx *c, const KspArgs &a, u32 n) {
+  constexpr size_t lds = lds_bytes<8, 16>();
+  const dim3 grid((1u << (LOG_N - 8)) / 16, n, c->K);
+  hipLaunchKernelGGL((ksp_fused_pass<LOG_N, KD, WIDE>), grid, dim3(256), lds, c->stream, a);
+  return fhe_check(c, hipGetLastError(), "ksp_fused_pass launch");
+}
+template <int LOG_N, int KD>
+int ksp_dispatch(fhe_ctx *c, const KspArgs &a, u32 n) {
+  return c->moduli[c->L] < (1ull << 60) ? ksp_launch<LOG_N, KD, true>(c, a, n) : ksp_launch<LOG_N, KD, false>(c, a, n);
+}
 
 // The fused finish applies: special moduli, N = 2^15 or 2^16 (a 256-point row
 // pass), at most 3 digits, and the Q limbs in one lazy-schedule class.
@@ -244,7 +379,54 @@ bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig) {
   const bool wide = c->moduli[0] < (1ull << 60);
   for (u32 i = 1; i < c->L; ++i)
     if ((c->moduli[i] < (1ull << 60)) != wide) return false;
-  return true;
+  // the P side (ntt_ksp_fused_launch): one lazy-schedule class over the P limbs too
+  const bool pwide = c->moduli[c->L] < (1ull << 60);
+  for (u32 k = 1; k < c->K; ++k)
+    if ((c->moduli[c->L + k] < (1ull << 60)) != pwide) return false;
+  return c->K >= 1;
+}
+
+// INTT(acc_P) with the P limbs' ModUp row transforms and inner product fused
+// into its first pass (ksp_fused_pass), then its column pass (d_iscale), as
+// ntt_inv_ksp_launch leaves acc's P rows
+int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig) {
+  if (!ks_fused_finish_ok(c, ndig)) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused P-limb key switch: shape");
+  const u32 L = c->L, K = c->K, QP = L + K;
+  const size_t N = c->n;
+  const u32 per = 32767u;  // ciphertexts per launch (the column pass takes 2 polys per ct on gridDim.y)
+  for (u32 c0 = 0; c0 < n; c0 += per) {
+    const u32 nc = std::min(per, n - c0);
+    KspArgs k{};
+    k.acc = acc + (size_t)c0 * 2 * QP * N;
+    k.ext = ext + (size_t)c0 * ndig * QP * N;
+    k.ksk = ksk;
+    k.mods = c->d_mods;
+    k.twf = c->d_tw_fwd;
+    k.twi = c->d_tw_inv;
+    k.L = L;
+    k.QP = QP;
+    k.kQP = ctx_key_qp(c);
+    k.kshift = c->key_pshift;
+    k.ndig = ndig;
+    int rc;
+    if (c->log_n == 15) {
+      rc = ndig == 1 ? ksp_dispatch<15, 1>(c, k, nc) : ndig == 2 ? ksp_dispatch<15, 2>(c, k, nc)
+                                                                  : ksp_dispatch<15, 3>(c, k, nc);
+    } else {
+      rc = ndig == 1 ? ksp_dispatch<16, 1>(c, k, nc) : ndig == 2 ? ksp_dispatch<16, 2>(c, k, nc)
+                                                                  : ksp_dispatch<16, 3>(c, k, nc);
+    }
+    if (rc) return rc;
+    NttArgs a{};
+    a.map = LimbMap{k.acc, QP, K, L, QP, 0, 0, 2 * nc};
+    a.tw = c->d_tw_inv;
+    a.mods = c->d_mods;
+    a.ninv = c->d_ninv;
+    a.log_n = c->log_n;
+    a.scale = c->d_iscale;
+    if ((rc = ntt_col_plain(c, a, true, 2 * nc * K))) return rc;
+  }
+  return FHE_OK;
 }
 
 int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, const u64 *ksk, u32 ndig,

@@ -42,9 +42,8 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
     const int wq = wide_mode(c, aq.map), wp = wide_mode(c, ap.map);
     int rc;
     if (!q_rows) {
-      // the fused finish transforms the Q targets' rows itself (ntt_ksf.hip)
-      if ((rc = ntt_conv_col(c, a, n_jobs))) return rc;
-      rc = ap.map.cnt ? ntt_row_plain(c, ap, false, np * ap.map.cnt) : FHE_OK;
+      // the fused key switch transforms every target's rows itself (ntt_ksf.hip)
+      rc = ntt_conv_col(c, a, n_jobs);
     } else if (wq != 2 && wp != 2 && wq != wp && aq.map.cnt && ap.map.cnt) {
 #if MODUP_COL_SPLIT
       if ((rc = ntt_conv_col(c, aq, np * aq.map.cnt))) return rc;

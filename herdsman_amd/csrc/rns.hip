@@ -1040,7 +1040,8 @@ static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, 
   //      conversion in its first pass and the combine in its last
   //      (out = base + (acc_Q - conv) P^-1): conv never makes an HBM round trip
   if (ntt_form && c->fuse_moddown) {
-    if (ksq && KSP_FUSE) rc = ntt_inv_ksp_launch(c, acc, ext, ksk, n, ndig, ext_g);
+    if (tsrc && tsrc->fused) rc = ntt_ksp_fused_launch(c, acc, ext, ksk, n, ndig);
+    else if (ksq && KSP_FUSE) rc = ntt_inv_ksp_launch(c, acc, ext, ksk, n, ndig, ext_g);
     else rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale);
     if (rc) return rc;
     if (tsrc && !(ksq && KSP_FUSE)) return fhe_fail(c, FHE_ERR_INVALID, "split tensor product without EPI_KSQ");
