@@ -74,7 +74,7 @@ struct KsfArgs {
 
 // ROT: a CKKS rotation's finish instead: the own digit's word is sigma_g(c1) R
 // and the base sigma_g(c0) (poly 0 only), both gathered from the ciphertext
-template <int LOG_N, int KD, bool WIDE, bool ROT>
+template <int LOG_N, int KD, bool WIDE, bool ROT, bool SP>
 __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
   constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
   using G0 = Grp<S, LOGR, 0>;
@@ -126,7 +126,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     u64 t[16];
     G0::template load_tw<S0>(t, tw, row, ts);
-    run_group<S, LOGR, 0, S0, false, true, WIDE, KSF_LSW>(x, t, q2, mi);
+    run_group<S, LOGR, 0, S0, false, SP, WIDE, KSF_LSW>(x, t, q2, mi);
     G1::template load_tw<S0>(t, tw, row, ts);
     const u32 l0 = lds_idx<S>(w, G0::k_thr(ts));
 #pragma unroll
@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
     const u32 l1 = lds_idx<S>(w, G1::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))];
-    run_group<S, LOGR, 1, S0, false, true, WIDE, KSF_LSW>(x, t, q2, mi);
+    run_group<S, LOGR, 1, S0, false, SP, WIDE, KSF_LSW>(x, t, q2, mi);
 #pragma unroll
     for (int r = 0; r < R; ++r) lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))] = x[r];
     __syncthreads();
@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
   // 1. the own digit (d2 R from a1 b1) and the base times P, canonical sums below 2q
   u64 acc0[R], acc1[R];
   if constexpr (ROT) {
-    const u64 pr = csub(mont_mul<true>(a.pr2[limb], 1, mi), q);  // P R
+    const u64 pr = csub(mont_mul<SP>(a.pr2[limb], 1, mi), q);  // P R
     const u64 *k0 = kb + jown * kj, *k1 = k0 + kbs;
     sfor<R / 2>([&](auto I) {
       constexpr int r = 2 * decltype(I)::value;
@@ -158,13 +158,13 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
       for (int h = 0; h < 2; ++h) {
         const u32 src = aut_src<LOG_N>((vio >> 3) + kr + h, a.g);
         const u64 y0 = ld_b(a0, src), y1 = ld_b(a1, src);  // sigma_g(c0), sigma_g(c1)
-        const u64 e = mont_mul<true>(y1, mi.r2, mi);        // sigma_g(c1) R, < 1.5q
-        acc0[r + h] = harvey_csub(mont_mul<true>(e, K0[h], mi) + mont_mul<true>(y0, pr, mi), nq2);
-        acc1[r + h] = mont_mul<true>(e, K1[h], mi);
+        const u64 e = mont_mul<SP>(y1, mi.r2, mi);        // sigma_g(c1) R, < 1.5q
+        acc0[r + h] = harvey_csub(mont_mul<SP>(e, K0[h], mi) + mont_mul<SP>(y0, pr, mi), nq2);
+        acc1[r + h] = mont_mul<SP>(e, K1[h], mi);
       }
     });
   } else {
-    const u64 r3 = csub(mont_mul<true>(mi.r2, mi.r2, mi), q);  // R^3
+    const u64 r3 = csub(mont_mul<SP>(mi.r2, mi.r2, mi), q);  // R^3
     const u64 pr2 = a.pr2[limb];
     const u64 *k0 = kb + jown * kj, *k1 = k0 + kbs;
     sfor<R / 2>([&](auto I) {
@@ -176,13 +176,13 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const u64 x0 = A0[h], x1 = A1[h], y0 = B0[h], y1 = B1[h];
-        const u64 e = mont_mul<true>(mont_reduce<true>(mul128(x1, y1), mi), r3, mi);        // d2 R, < 1.5q
-        const u64 d0p = mont_mul<true>(mont_reduce<true>(mul128(x0, y0), mi), pr2, mi);    // base_0 P
+        const u64 e = mont_mul<SP>(mont_reduce<SP>(mul128(x1, y1), mi), r3, mi);        // d2 R, < 1.5q
+        const u64 d0p = mont_mul<SP>(mont_reduce<SP>(mul128(x0, y0), mi), pr2, mi);    // base_0 P
         U128 t1 = mul128(x0, y1);
         mac128(t1, x1, y0);
-        const u64 d1p = mont_mul<true>(mont_reduce<true>(t1, mi), pr2, mi);                // base_1 P
-        acc0[r + h] = harvey_csub(mont_mul<true>(e, K0[h], mi) + d0p, nq2);
-        acc1[r + h] = harvey_csub(mont_mul<true>(e, K1[h], mi) + d1p, nq2);
+        const u64 d1p = mont_mul<SP>(mont_reduce<SP>(t1, mi), pr2, mi);                // base_1 P
+        acc0[r + h] = harvey_csub(mont_mul<SP>(e, K0[h], mi) + d0p, nq2);
+        acc1[r + h] = harvey_csub(mont_mul<SP>(e, K1[h], mi) + d1p, nq2);
       }
     });
   }
@@ -200,8 +200,8 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
       const u64x2 K0 = ld2_b(k0 + kr, vio), K1 = ld2_b(k1 + kr, vio);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        acc0[r + h] = harvey_csub(acc0[r + h] + mont_mul<true>(x[r + h], K0[h], mi), nq2);
-        acc1[r + h] = harvey_csub(acc1[r + h] + mont_mul<true>(x[r + h], K1[h], mi), nq2);
+        acc0[r + h] = harvey_csub(acc0[r + h] + mont_mul<SP>(x[r + h], K0[h], mi), nq2);
+        acc1[r + h] = harvey_csub(acc1[r + h] + mont_mul<SP>(x[r + h], K1[h], mi), nq2);
       }
     });
   }
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
       for (int h = 0; h < 2; ++h) {
         const u64 v = harvey_csub(x[r + h], WIDE ? nq4 : nq2);  // below 4q (WIDE) / 2q
         const u64 s = harvey_csub(acc[r + h], nq1);
-        o[h] = harvey_csub(mont_mul<true>((s + cb1) + ~v, pinv, mi), nq1);
+        o[h] = harvey_csub(mont_mul<SP>((s + cb1) + ~v, pinv, mi), nq1);
       }
       st2_e(ob + IO::k_reg(r), vio, u64x2{o[0], o[1]});
     });
@@ -236,7 +236,8 @@ template <int LOG_N, int KD, bool WIDE, bool ROT>
 int ksf_launch(fhe_ctx *c, const KsfArgs &a, u32 n) {
   constexpr size_t lds = lds_bytes<8, 16>();
   const dim3 grid((1u << (LOG_N - 8)) / 16, n, a.L);
-  hipLaunchKernelGGL((ksf_pass<LOG_N, KD, WIDE, ROT>), grid, dim3(256), lds, c->stream, a);
+  if (c->special) hipLaunchKernelGGL((ksf_pass<LOG_N, KD, WIDE, ROT, true>), grid, dim3(256), lds, c->stream, a);
+  else hipLaunchKernelGGL((ksf_pass<LOG_N, KD, WIDE, ROT, false>), grid, dim3(256), lds, c->stream, a);
   return fhe_check(c, hipGetLastError(), "ksf_pass launch");
 }
 
@@ -252,7 +253,7 @@ int ksf_dispatch(fhe_ctx *c, const KsfArgs &a, u32 n) {
 // (they are all non-own), forms acc_P,b = sum_j ext_j ksk_j,b R^-1 for b = 0, 1
 // and runs the first (row) pass of INTT(acc_P,b) on it, so the ModUp row pass
 // and PRO_KSP's ext reads go away; the INTT's column pass follows as before.
-template <int LOG_N, int KD, bool WIDE>
+template <int LOG_N, int KD, bool WIDE, bool SP>
 __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
   constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
   using G0 = Grp<S, LOGR, 0>;
@@ -287,7 +288,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     u64 t[16];
     G0::template load_tw<S0>(t, twf, row, ts);
-    run_group<S, LOGR, 0, S0, false, true, WIDE, KSP_LSW>(x, t, q2, mi);
+    run_group<S, LOGR, 0, S0, false, SP, WIDE, KSP_LSW>(x, t, q2, mi);
     G1::template load_tw<S0>(t, twf, row, ts);
     const u32 l0 = lds_idx<S>(w, G0::k_thr(ts));
 #pragma unroll
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
     const u32 l1 = lds_idx<S>(w, G1::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))];
-    run_group<S, LOGR, 1, S0, false, true, WIDE, KSP_LSW>(x, t, q2, mi);
+    run_group<S, LOGR, 1, S0, false, SP, WIDE, KSP_LSW>(x, t, q2, mi);
 #pragma unroll
     for (int r = 0; r < R; ++r) lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))] = x[r];
     __syncthreads();
@@ -322,8 +323,8 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
       const u64x2 K0 = ld2_b(k0 + kr, vio), K1 = ld2_b(k1 + kr, vio);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        acc0[r + h] = harvey_csub(acc0[r + h] + mont_mul<true>(x[r + h], K0[h], mi), nq2);
-        acc1[r + h] = harvey_csub(acc1[r + h] + mont_mul<true>(x[r + h], K1[h], mi), nq2);
+        acc0[r + h] = harvey_csub(acc0[r + h] + mont_mul<SP>(x[r + h], K0[h], mi), nq2);
+        acc1[r + h] = harvey_csub(acc1[r + h] + mont_mul<SP>(x[r + h], K1[h], mi), nq2);
       }
     });
   }
@@ -341,7 +342,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
     const u32 l1 = lds_idx<S>(w, G1::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))];
-    run_group<S, LOGR, 1, S0, true, true, false, KSP_LSW>(x, t, q2, mi);
+    run_group<S, LOGR, 1, S0, true, SP, false, KSP_LSW>(x, t, q2, mi);
     G0::template load_tw<S0>(t, twi, row, ts);
 #pragma unroll
     for (int r = 0; r < R; ++r) lds[l1 + G1::k_reg(r) + lds_pad(G1::k_reg(r))] = x[r];
@@ -349,7 +350,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
     const u32 l0 = lds_idx<S>(w, G0::k_thr(ts));
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = lds[l0 + G0::k_reg(r) + lds_pad(G0::k_reg(r))];
-    run_group<S, LOGR, 0, S0, true, true, false, KSP_LSW>(x, t, q2, mi);
+    run_group<S, LOGR, 0, S0, true, SP, false, KSP_LSW>(x, t, q2, mi);
     u64 *dst = a.acc + ((size_t)(2 * ct + b) * a.QP + limb) * N;
 #pragma unroll
     for (int r = 0; r < R; ++r) st_d(dst + G0::k_reg(r), vst, x[r]);
@@ -364,7 +365,8 @@ template <int LOG_N, int KD, bool WIDE>
 int ksp_launch(fhe_ctx *c, const KspArgs &a, u32 n) {
   constexpr size_t lds = lds_bytes<8, 16>();
   const dim3 grid((1u << (LOG_N - 8)) / 16, n, c->K);
-  hipLaunchKernelGGL((ksp_fused_pass<LOG_N, KD, WIDE>), grid, dim3(256), lds, c->stream, a);
+  if (c->special) hipLaunchKernelGGL((ksp_fused_pass<LOG_N, KD, WIDE, true>), grid, dim3(256), lds, c->stream, a);
+  else hipLaunchKernelGGL((ksp_fused_pass<LOG_N, KD, WIDE, false>), grid, dim3(256), lds, c->stream, a);
   return fhe_check(c, hipGetLastError(), "ksp_fused_pass launch");
 }
 template <int LOG_N, int KD>
@@ -372,10 +374,10 @@ int ksp_dispatch(fhe_ctx *c, const KspArgs &a, u32 n) {
   return c->moduli[c->L] < (1ull << 60) ? ksp_launch<LOG_N, KD, true>(c, a, n) : ksp_launch<LOG_N, KD, false>(c, a, n);
 }
 
-// The fused finish applies: special moduli, N = 2^15 or 2^16 (a 256-point row
-// pass), at most 3 digits, and the Q limbs in one lazy-schedule class.
+// The fused finish applies: N = 2^15 or 2^16 (a 256-point row pass), at most 3
+// digits, the Q limbs in one lazy-schedule class and the P limbs in one.
 bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig) {
-  if (!KSF_FUSE || !c->special || (c->log_n != 15 && c->log_n != 16) || ndig < 1 || ndig > 3 || !c->L) return false;
+  if (!KSF_FUSE || (c->log_n != 15 && c->log_n != 16) || ndig < 1 || ndig > 3 || !c->L) return false;
   const bool wide = c->moduli[0] < (1ull << 60);
   for (u32 i = 1; i < c->L; ++i)
     if ((c->moduli[i] < (1ull << 60)) != wide) return false;

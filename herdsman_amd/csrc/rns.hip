@@ -1155,11 +1155,15 @@ int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, 
   if (rc) return rc;
   const KsWs w = ks_layout(c, n, (u64 *)ws);
   const size_t bytes = sizeof(u64) * 2 * c->L * c->n * (size_t)n;
-  // (special moduli: the generic-product EPI_KSQT keeps its operand ring in scratch, -18%)
-  const bool split = TENSOR_SPLIT && c->special && c->log_n > 14 && c->fuse_moddown && w.ndig <= 3 && KSP_FUSE &&
-                     !ranges_overlap(out, a, bytes) && !ranges_overlap(out, b, bytes);
+  // the fused key switch (ntt_ksf.hip) where it applies; else the split finish
+  // EPI_KSQT on special moduli only (the generic-product EPI_KSQT keeps its
+  // operand ring in scratch, -18%)
+  const bool apart = !ranges_overlap(out, a, bytes) && !ranges_overlap(out, b, bytes);
+  const bool pre = TENSOR_SPLIT && c->log_n > 14 && c->fuse_moddown && w.ndig <= 3 && KSP_FUSE && apart;
+  const bool fused = pre && c->fuse_modup && ks_fused_finish_ok(c, w.ndig);
+  const bool split = fused || (pre && c->special);
   if ((rc = ntt_inv_tensor_launch(c, a, b, out, w.dc, w.ext, n, w.ndig, split))) return rc;
-  const TensorSrc ts{a, b, split && c->fuse_modup && ks_fused_finish_ok(c, w.ndig)};
+  const TensorSrc ts{a, b, fused};
   return keyswitch_run(c, w, rlk, out, out, n, 3u, true, true, 0, split ? &ts : nullptr);
 }
 
