@@ -13,8 +13,9 @@
 //   3. for b = 0, 1: the row transform of NTT(conv_b)'s intermediate and the
 //      ModDown finish out_b = (acc_b - conv_b) P^-1 = base_b + (acc_b' - conv_b) P^-1
 // so ext's Q limbs are never stored (the P limbs: ksp_fused_pass below; with
-// both, ntt_fwd_modup_launch runs ModUp's column passes only).  The two accumulators (32 words per thread)
-// stay in registers across the four row transforms: 3 waves per SIMD.
+// both, ntt_fwd_modup_launch runs ModUp's column passes only).  The two
+// accumulators (32 words per thread) stay in registers across the four row
+// transforms: 3 waves per SIMD.
 // A rotation (ROT) runs the same finish with the own digit's word sigma_g(c1) R
 // and the base sigma_g(c0) (poly 0) gathered from the ciphertext, so
 // PRO_AUTOMORPH stores neither.
@@ -29,7 +30,7 @@
 #define KSF_LSW 4  // butterflies per lock-step chunk (run_group LSW): 8 needs more temporaries than the accumulators leave
 #endif
 #ifndef KSP_LSW
-#define KSP_LSW 2  // the same for the P side (ksp_fused_pass: 4 spills 11 VGPRs)
+#define KSP_LSW 2  // the same for the P side (6-9 VGPRs spill, outside the loops: addresses for the INTT phase)
 #endif
 #ifndef KSF_MINW
 #define KSF_MINW 3  // minimum waves per SIMD (the accumulators take 64 VGPRs)
@@ -73,7 +74,8 @@ struct KsfArgs {
 };
 
 // ROT: a CKKS rotation's finish instead: the own digit's word is sigma_g(c1) R
-// and the base sigma_g(c0) (poly 0 only), both gathered from the ciphertext
+// and the base sigma_g(c0) (poly 0 only), both gathered from the ciphertext.
+// SP: the special-modulus Montgomery product (q = 1 mod 2^32), else the generic one.
 template <int LOG_N, int KD, bool WIDE, bool ROT, bool SP>
 __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
   constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
