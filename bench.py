@@ -281,11 +281,14 @@ def main():
     limbs = B * 3 * L
     x = hb.empty((B * 3, L, n), device=dev)
     ctx.fill_uniform(x, seed=99)
+    if world > 1:
+        # every rank's NTT loop runs at the same time (the N-GPU NTT/s); the barrier
+        # comes BEFORE the warm-up launches, so no rank idles (and re-ramps its clock)
+        # between them and the timed ones
+        torch.cuda.synchronize(dev)
+        dist.barrier()
     for _ in range(3):
         ctx.ntt_fwd(x)
-    if world > 1:
-        torch.cuda.synchronize(dev)
-        dist.barrier()  # every rank's NTT loop runs at the same time (the N-GPU NTT/s)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)  # the stream the NTT kernels are launched on (ctx.set_stream above)
     reps = max(1, args.ntt_reps)

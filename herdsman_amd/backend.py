@@ -8,6 +8,7 @@ call raises FheBackendError.
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 from typing import Optional, Sequence
 
@@ -50,6 +51,7 @@ SIGNATURES = {
     "fhe_ctx_create": (C.c_int, [C.POINTER(_Params), C.c_int, C.POINTER(_vp)]),
     "fhe_ctx_destroy": (None, [_vp]),
     "fhe_last_error": (C.c_char_p, [_vp]),
+    "fhe_build_id": (C.c_char_p, []),
     "fhe_ctx_moduli": (C.c_int, [_vp, _vp, _u32, C.POINTER(_u32)]),
     "fhe_set_stream": (C.c_int, [_vp, _vp]),
     "fhe_synchronize": (C.c_int, [_vp]),
@@ -112,8 +114,41 @@ def library_path() -> str:
     return os.environ.get("HERD_FHE_LIB") or os.path.join(HERE, "lib", "libherdsman_fhe.so")
 
 
+def source_build_id(root: str = HERE) -> Optional[str]:
+    """SHA-256 of the library's sources as the Makefile bakes it into
+    fhe_build_id(): every file of csrc/ and include/plugins/fhe_backend.h, in
+    sorted relative-path order, contents concatenated.  None if the sources are
+    not there (an installed copy without them)."""
+    csrc = os.path.join(root, "csrc")
+    hdr = os.path.join(root, "..", "include", "plugins", "fhe_backend.h")
+    if not os.path.isdir(csrc) or not os.path.exists(hdr):
+        return None
+    rel = ["csrc/" + f for f in os.listdir(csrc) if os.path.isfile(os.path.join(csrc, f))]
+    rel.append("../include/plugins/fhe_backend.h")
+    h = hashlib.sha256()
+    for r in sorted(rel):
+        with open(os.path.join(root, r), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def check_build_id(lib, root: str = HERE) -> str:
+    """Refuse a library whose baked-in build id does not match the sources
+    under `root` (a stale .so next to newer sources).  Returns the id."""
+    if not hasattr(lib, "fhe_build_id"):
+        raise FheBackendError("library exports no fhe_build_id(): rebuild it (make -C herdsman_amd)")
+    lib.fhe_build_id.restype, lib.fhe_build_id.argtypes = C.c_char_p, []
+    built = lib.fhe_build_id().decode()
+    want = source_build_id(root)
+    if want is not None and built != want:
+        raise FheBackendError(f"libherdsman_fhe.so was built from other sources (build id {built[:16]}, "
+                              f"sources {want[:16]}): rebuild it (make -C herdsman_amd)")
+    return built
+
+
 def load_library():
-    """Load the HIP backend; raises (never falls back) when it is missing."""
+    """Load the HIP backend; raises (never falls back) when it is missing or
+    was built from sources other than the ones checked out."""
     global _lib
     if _lib is not None:
         return _lib
@@ -122,6 +157,8 @@ def load_library():
         raise FheBackendError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = C.CDLL(path)
     variant = bool(os.environ.get("HERD_FHE_LIB"))
+    if not variant:  # an A/B variant is built from modified sources on purpose
+        check_build_id(lib)
     for name, (res, args) in SIGNATURES.items():
         if variant and not hasattr(lib, name):
             continue  # an older build under A/B may predate an entry point it is not asked for

@@ -20,6 +20,9 @@
 #include <cstring>
 #include <fstream>
 #include <list>
+#include <set>
+#include <type_traits>
+#include <variant>
 #include <exception>
 #include <stdexcept>
 #include <string>
@@ -484,6 +487,12 @@ struct ResidentFrame {
   // the device budget this frame's bytes are charged to (cleared when it is
   // evicted; the memory itself goes when the last reader drops the frame)
   FrameBudget *budget = nullptr;
+  // identity of the partition file once it is committed (size, mtime): a
+  // lookup that finds the file changed under it (rewritten outside this group)
+  // drops the HBM copy instead of serving stale rows
+  bool file_known = false;
+  uintmax_t file_size = 0;
+  std::filesystem::file_time_type file_mtime{};
   ~ResidentFrame();
 };
 
@@ -528,6 +537,12 @@ struct GpuWorkerGroup::Frames {
   std::deque<std::shared_ptr<ResidentFrame>> queue;              // waiting for the flusher
   std::map<std::string, std::shared_ptr<ResidentFrame>> pending;  // queued or being written
   bool stop = false, failed = false;
+  // write-behind failures: frame key -> error, until the partition is rewritten
+  // (every task that reads the key completes with ERROR), and the sessions
+  // whose next scheduled task reports the failure (executor.cpp:168-178 then
+  // fails the job)
+  std::map<std::string, std::string> flush_failed;
+  std::set<std::string> failed_sessions;
   std::map<std::tuple<uint32_t, int, int>, fhe_ctx *> flush_ctx;  // (flusher, device, schema) -> its context
   StageStats st;                                      // flushed rows and time
 
@@ -537,6 +552,11 @@ struct GpuWorkerGroup::Frames {
     std::lock_guard lk(m);
     FrameBudget &b = dev[device];
     if (need > cap) return nullptr;
+    // bytes reserved for outputs still being produced cannot be evicted: evict
+    // only when the published frames free enough for the reservation to fit
+    uint64_t evictable = 0;
+    for (const auto &kv : b.map) evictable += kv.second->bytes();
+    if (b.bytes - evictable + need > cap) return nullptr;
     while (b.bytes + need > cap && !b.lru.empty()) {
       auto it = b.map.find(b.lru.back());
       b.lru.pop_back();
@@ -564,8 +584,13 @@ struct GpuWorkerGroup::Frames {
     b.lru.push_front(f->key);
   }
   // the partition is being rewritten: no device may serve its old contents
+  // (a failed write-behind of the old contents no longer matters)
   void drop(const std::string &key, std::vector<std::shared_ptr<ResidentFrame>> &dropped) {
     std::lock_guard lk(m);
+    flush_failed.erase(key);
+    drop_locked(key, dropped);
+  }
+  void drop_locked(const std::string &key, std::vector<std::shared_ptr<ResidentFrame>> &dropped) {
     for (auto &kv : dev) {
       FrameBudget &b = kv.second;
       auto it = b.map.find(key);
@@ -577,11 +602,40 @@ struct GpuWorkerGroup::Frames {
       b.lru.remove(key);
     }
   }
+  // every frame whose key starts with `prefix` (a session's or a data frame's
+  // partitions): herdsman deleted them
+  void drop_prefix(const std::string &prefix, std::vector<std::shared_ptr<ResidentFrame>> &dropped) {
+    std::lock_guard lk(m);
+    std::set<std::string> keys;
+    for (auto &kv : dev)
+      for (auto &f : kv.second.map)
+        if (f.first.compare(0, prefix.size(), prefix) == 0) keys.insert(f.first);
+    for (const auto &k : keys) drop_locked(k, dropped);
+    for (auto it = flush_failed.begin(); it != flush_failed.end();)
+      it = it->first.compare(0, prefix.size(), prefix) == 0 ? flush_failed.erase(it) : std::next(it);
+  }
+  // free every published frame of the device (a device allocation failed)
+  void evict_all(int device, std::vector<std::shared_ptr<ResidentFrame>> &evicted) {
+    std::lock_guard lk(m);
+    FrameBudget &b = dev[device];
+    std::vector<std::string> keys(b.lru.begin(), b.lru.end());
+    for (const auto &k : keys) drop_locked(k, evicted);
+  }
   std::shared_ptr<ResidentFrame> lookup(int device, const std::string &key, int schema) {
+    std::vector<std::shared_ptr<ResidentFrame>> stale;  // freed after the lock is released
     std::lock_guard lk(m);
     FrameBudget &b = dev[device];
     auto it = b.map.find(key);
     if (it == b.map.end() || it->second->schema != schema) return nullptr;
+    if (it->second->file_known) {  // the committed file must still be the one this frame holds
+      std::error_code ec;
+      const uintmax_t sz = std::filesystem::file_size(it->second->file, ec);
+      const auto mt = ec ? std::filesystem::file_time_type{} : std::filesystem::last_write_time(it->second->file, ec);
+      if (ec || sz != it->second->file_size || mt != it->second->file_mtime) {
+        drop_locked(key, stale);
+        return nullptr;
+      }
+    }
     b.lru.remove(key);
     b.lru.push_front(key);
     return it->second;
@@ -591,7 +645,32 @@ struct GpuWorkerGroup::Frames {
     std::unique_lock lk(m);
     cv.wait(lk, [&] { return !pending.count(key); });
   }
+  // the error of a failed write-behind of `key`, or empty
+  std::string flush_error(const std::string &key) {
+    std::lock_guard lk(m);
+    auto it = flush_failed.find(key);
+    return it == flush_failed.end() ? std::string() : it->second;
+  }
+  // true once per failed write-behind of the session: its next task reports it
+  bool take_session_failure(const std::string &session) {
+    std::lock_guard lk(m);
+    return failed_sessions.erase(session) > 0;
+  }
 };
+
+namespace {
+// the committed file's identity, recorded in a frame that holds its contents
+void note_file(ResidentFrame &f) {
+  std::error_code ec;
+  const uintmax_t sz = std::filesystem::file_size(f.file, ec);
+  if (ec) return;
+  const auto mt = std::filesystem::last_write_time(f.file, ec);
+  if (ec) return;
+  f.file_size = sz;
+  f.file_mtime = mt;
+  f.file_known = true;
+}
+}  // namespace
 
 ResidentFrame::~ResidentFrame() {
   if (p) fhe_dev_free(ctx, p);
@@ -710,6 +789,11 @@ void GpuWorkerGroup::reset_stage_stats() {
   frames_->st = StageStats{};
 }
 
+void GpuWorkerGroup::drop_frames(const herd::common::UUID &session, const herd::common::UUID *frame) {
+  std::vector<std::shared_ptr<ResidentFrame>> dropped;
+  frames_->drop_prefix(session.as_string() + "/" + (frame ? frame->as_string() + "/" : std::string()), dropped);
+}
+
 bool GpuWorkerGroup::flush_frames() {
   std::unique_lock lk(frames_->m);
   frames_->cv.wait(lk, [&] { return frames_->queue.empty() && frames_->pending.empty(); });
@@ -726,6 +810,17 @@ std::shared_ptr<IWorkerGroup::TaskHandle> GpuWorkerGroup::schedule_task(const he
   auto h = std::make_shared<Handle>();
   if (std::holds_alternative<std::monostate>(task) || !circuits_lowerable()) {
     complete(h, Status::ERROR);  // delivered once the executor attaches its callback
+    return h;
+  }
+  const std::string session =
+      std::visit([](const auto &t) -> std::string {
+        if constexpr (std::is_same_v<std::decay_t<decltype(t)>, std::monostate>) return std::string();
+        else return t.session_uuid.as_string();
+      }, task);
+  if (frames_->take_session_failure(session)) {
+    std::fprintf(stderr, "GpuWorkerGroup: session %s: a partition written behind failed to commit; task fails\n",
+                 session.c_str());
+    complete(h, Status::ERROR);
     return h;
   }
   Device &d = *devices_[next_device_.fetch_add(1) % devices_.size()];  // round robin, like grpc_worker_group.cpp:102
@@ -1248,8 +1343,11 @@ void GpuWorkerGroup::flush_loop(uint32_t id) {
       frames_->st.flush_s += secs_since(t0);
       if (err.empty()) {
         frames_->st.flushed_rows += f->rows;
+        note_file(*f);
       } else {
         frames_->failed = true;
+        frames_->flush_failed[f->key] = err;
+        frames_->failed_sessions.insert(f->key.substr(0, f->key.find('/')));
         std::fprintf(stderr, "GpuWorkerGroup: write-behind of %s failed: %s\n", f->file.c_str(), err.c_str());
       }
     }
@@ -1285,11 +1383,16 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         const auto out_path = frame_path(config_.storage_dir, t.session_uuid, t.output_data_frame_ptr);
         std::vector<std::shared_ptr<ResidentFrame>> released;  // freed outside the frames lock
         frames_->drop(out_key, released);  // the output partition is rewritten: no stale copy stays
+        frames_->wait_file(out_key);       // nor may an older flush of it commit after this task's file
         MapIo io;
         std::unique_ptr<PartitionIndex> in_file;
         io.in = frames_->lookup(dev.id, in_key, schema);
         if (!io.in) {
           frames_->wait_file(in_key);  // a file still being written behind
+        }
+        if (const std::string e = frames_->flush_error(in_key); !e.empty())
+          throw std::runtime_error("input partition " + in_key + " was never committed (write-behind failed: " + e + ")");
+        if (!io.in) {
           in_file = std::make_unique<PartitionIndex>(
               frame_path(config_.storage_dir, t.session_uuid, t.input_data_frame_ptr.pointer));
           io.rows = in_file.get();
@@ -1324,7 +1427,14 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
             f->header = ct_header(s, lvl);
             f->durable = config_.durable_outputs;
             void *q = nullptr;
-            if (fhe_dev_alloc(s.ctx, f->bytes(), &q) == FHE_OK) {
+            int arc = fhe_dev_alloc(s.ctx, f->bytes(), &q);
+            if (arc == FHE_ERR_OOM) {  // idle frames give way before the output falls back to its file
+              std::vector<std::shared_ptr<ResidentFrame>> evicted;
+              frames_->evict_all(dev.id, evicted);
+              evicted.clear();
+              arc = fhe_dev_alloc(s.ctx, f->bytes(), &q);
+            }
+            if (arc == FHE_OK) {
               f->p = static_cast<uint64_t *>(q);
               io.out = std::move(f);
             } else {
@@ -1358,6 +1468,7 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         }
         if (pending >= 0) finish_map_batch(ls, pending, out.get(), config_.io_threads, stats);
         if (out) out->commit();
+        if (io.out && io.write_file) note_file(*io.out);
         if (io.out) {
           // every batch's copy into the frame has completed (the last mark);
           // from here a task on any lane of this device reads it from HBM
@@ -1387,7 +1498,9 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         if (mul) ks = device_keys(dev.keys_m, dev.keys, s, config_.key_dir, t.session_uuid.as_string(), schema);
         {
           std::vector<std::shared_ptr<ResidentFrame>> released;
-          frames_->drop(frame_key(t.session_uuid, t.output_data_frame_ptr), released);
+          const std::string out_key = frame_key(t.session_uuid, t.output_data_frame_ptr);
+          frames_->drop(out_key, released);
+          frames_->wait_file(out_key);
         }
         // each input partition from HBM when a Map stage on this device left it
         // resident, else from its file
@@ -1402,10 +1515,11 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
           Input pi;
           const std::string key = frame_key(t.session_uuid, in.pointer);
           pi.res = frames_->lookup(dev.id, key, schema);
-          if (!pi.res) {
-            frames_->wait_file(key);
+          if (!pi.res) frames_->wait_file(key);
+          if (const std::string e = frames_->flush_error(key); !e.empty())
+            throw std::runtime_error("input partition " + key + " was never committed (write-behind failed: " + e + ")");
+          if (!pi.res)
             pi.file = std::make_unique<PartitionIndex>(frame_path(config_.storage_dir, t.session_uuid, in.pointer));
-          }
           count += pi.size();
           parts.push_back(std::move(pi));
         }
@@ -1510,8 +1624,9 @@ void GpuWorkerGroup::lane_loop(Device &dev, Lane &lane) {
         out.append({{&h, sizeof(h)}, {res, cw * 8}});
         out.commit();
       }
-    } catch (const std::exception &) {
+    } catch (const std::exception &e) {
       st = Status::ERROR;  // no exception crosses the seam (executor.cpp:168-178 fails the job)
+      std::fprintf(stderr, "GpuWorkerGroup: task failed: %s\n", e.what());
       // copies of this task may still be reading or filling the lane's pinned
       // buffers: let them finish before the next task reuses (or regrows) them
       if (cur) (void)fhe_synchronize(cur->s.ctx);

@@ -104,7 +104,11 @@ struct GpuWorkerGroupConfig {
   // herdsman chains Map stages through intermediate-<job>-<node> frames that the
   // next stage reads back (execution_service.cpp:525-543), which is the case this
   // serves.  The partition file is still written (the storage contract holds).
-  uint64_t resident_frame_bytes = 16ull << 30;
+  // Off by default: the budget is the deployer's share of HBM beside the
+  // contexts, keys and workspaces (one budget per group per device).  A failed
+  // device allocation evicts the frames first; a frame whose committed file
+  // changed on disk (size or mtime) is dropped at lookup, not served.
+  uint64_t resident_frame_bytes = 0;
   // write_behind: a MapTask whose output is resident completes once that output
   // is in HBM, and the group's flusher thread writes the partition file behind
   // it (D2H + file writes off the lanes).  flush_frames() returns once every
@@ -126,7 +130,13 @@ class GpuWorkerGroup : public IWorkerGroup {
   void reset_stage_stats();
   // write_behind: block until every partition file queued so far is committed;
   // false if a flush failed (its message on stderr).  No-op otherwise.
+  // A failed flush also fails every later task that reads that partition, and
+  // the session's next scheduled task, with Status::ERROR (the executor then
+  // fails the job, executor.cpp:168-178).
   bool flush_frames();
+  // herdsman deleted a data frame (frame != nullptr) or a whole session: its
+  // resident frames go now, not when another frame needs the budget
+  void drop_frames(const herd::common::UUID &session, const herd::common::UUID *frame = nullptr);
   // false when herd_common's Circuit has no lowering to the backend's ops
   // (under HERDSMAN_REAL_SEAM): the group then fails every task at once
   static bool circuits_lowerable() noexcept;

@@ -81,6 +81,10 @@ typedef struct fhe_params {
 int fhe_ctx_create(const fhe_params *params, int device, fhe_ctx **out);
 void fhe_ctx_destroy(fhe_ctx *ctx);
 const char *fhe_last_error(const fhe_ctx *ctx);
+/* SHA-256 (hex) of the sources this library was built from (herdsman_amd/csrc/
+ * and this header, herdsman_amd/Makefile), so a loader can refuse a library
+ * that does not match the sources it was shipped with */
+const char *fhe_build_id(void);
 /* number of moduli in the index space, and the moduli themselves (HOST out) */
 int fhe_ctx_moduli(const fhe_ctx *ctx, uint64_t *out, uint32_t cap, uint32_t *count);
 int fhe_set_stream(fhe_ctx *ctx, void *hip_stream);

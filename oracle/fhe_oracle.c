@@ -858,6 +858,16 @@ void orc_mul_relin(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const
   free(H);
 }
 
+/* The checker refuses what it does not implement, as the GPU ABI does
+ * (fhe_backend.cpp ctx_level / ew_level_ok): BFV ciphertexts live at level L
+ * only, and the level-lvl entries below compute the CKKS product and rescale.
+ * Returns 0, or ORC_ERR_UNSUPPORTED / ORC_ERR_INVALID without touching out. */
+static int level_ok(const orc_ctx *c, uint32_t lvl, int ckks_only) {
+  if (lvl < 1 || lvl > c->L) return ORC_ERR_INVALID;
+  if (c->scheme == ORC_SCHEME_BFV && (ckks_only || lvl != c->L)) return ORC_ERR_UNSUPPORTED;
+  return 0;
+}
+
 static void rotate_lvl(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
                        uint32_t n_ct, uint32_t lvl) {
   const size_t L = lvl, N = c->n, CT = 2 * L * N;
@@ -910,9 +920,12 @@ void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, co
 }
 
 /* the same at level lvl: ct, outs [..][2][lvl][N], full-level keys */
-void orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
-                           const uint64_t *gks, uint64_t *outs, uint32_t n_ct, uint32_t lvl) {
+int orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                          const uint64_t *gks, uint64_t *outs, uint32_t n_ct, uint32_t lvl) {
+  const int rc = level_ok(c, lvl, 0);
+  if (rc) return rc;
   rotate_hoisted_lvl(c, ct, n_rot, galois, gks, outs, n_ct, lvl);
+  return 0;
 }
 
 /* Double-hoisted rotation sum (Bossuat et al.'s hoisted ModDown): out = sum_r
@@ -920,8 +933,10 @@ void orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot,
  * Q u P before ONE ModDown, plus sum_r sigma_{g_r}(c0).  Decrypts to the sum of
  * the rotated messages; the bits differ from summing hoisted rotations by the
  * ModDown rounding.  out [n_ct][2][lvl][N]. */
-void orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
-                               const uint64_t *gks, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+int orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                              const uint64_t *gks, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+  const int rc = level_ok(c, lvl, 0);
+  if (rc) return rc;
   const size_t L = lvl, N = c->n, CT = 2 * L * N, KW = (size_t)c->dnum * 2 * (c->L + c->K) * N;
   const int ckks = c->scheme == ORC_SCHEME_CKKS;
   const uint64_t **ks_r = malloc(sizeof(uint64_t *) * (n_rot ? n_rot : 1));
@@ -940,14 +955,17 @@ void orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_
     free(ks); free(rot);
   }
   free(ks_r);
+  return 0;
 }
 
 /* Hoisted linear transform (CKKS): out = sum_r pts[r] (.) rot_{g_r}(ct), the
  * plaintext-weighted inner products of every element summed in Q u P before
  * ONE ModDown, plus sum_r pts[r] (.) sigma_{g_r}(c0).  pts [n_rot][L+K][N] in
  * the NTT domain (full-level rows; a level uses rows 0..lvl-1 and L..L+K-1). */
-void orc_linear_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
-                           const uint64_t *gks, const uint64_t *pts, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+int orc_linear_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+                          const uint64_t *gks, const uint64_t *pts, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+  const int rc = level_ok(c, lvl, 1);
+  if (rc) return rc;
   const size_t L = lvl, N = c->n, CT = 2 * L * N, KW = (size_t)c->dnum * 2 * (c->L + c->K) * N;
   const size_t PW = (size_t)(c->L + c->K) * N;
   const uint64_t **ks_r = malloc(sizeof(uint64_t *) * (n_rot ? n_rot : 1));
@@ -972,26 +990,40 @@ void orc_linear_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot,
     free(ks); free(rot);
   }
   free(ks_r); free(pt_r);
+  return 0;
 }
 
 /* ------------------------------------------------- CKKS levels (rescale) */
-void orc_keyswitch_at(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
-                      uint32_t lvl) {
+int orc_keyswitch_at(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
+                     uint32_t lvl) {
+  const int rc = level_ok(c, lvl, 0);
+  if (rc) return rc;
   const size_t N = c->n;
   for (uint32_t i = 0; i < n; ++i)
     keyswitch_lvl(c, d + i * lvl * N, ksk, out + i * 2 * lvl * N, c->scheme == ORC_SCHEME_CKKS, lvl);
+  return 0;
 }
 
-void orc_mul_relin_at(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
-                      uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+int orc_mul_relin_at(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
+                     uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+  const int rc = level_ok(c, lvl, 0);
+  if (rc) return rc;
+  if (c->scheme == ORC_SCHEME_BFV) { /* level L: the BFV product, as fhe_mul_relin_at's full-level context */
+    orc_mul_relin(c, a, b, rlk, out, n_ct);
+    return 0;
+  }
   const size_t CT = 2 * (size_t)lvl * c->n;
 #pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
   for (long i = 0; i < (long)n_ct; ++i) ckks_mul_relin_one(c, a + i * CT, b + i * CT, rlk, out + i * CT, lvl);
+  return 0;
 }
 
-void orc_rotate_at(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
-                   uint32_t n_ct, uint32_t lvl) {
+int orc_rotate_at(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint64_t *gk, uint64_t *out,
+                  uint32_t n_ct, uint32_t lvl) {
+  const int rc = level_ok(c, lvl, 0);
+  if (rc) return rc;
   rotate_lvl(c, ct, g, gk, out, n_ct, lvl);
+  return 0;
 }
 
 /* CKKS rescale (OpenFHE DCRTPoly::DropLastElementAndScale, SEAL
@@ -999,7 +1031,10 @@ void orc_rotate_at(const orc_ctx *c, const uint64_t *ct, uint32_t g, const uint6
  * lifted centrally (x - q_{l-1} if x > q_{l-1}/2, the same value both
  * libraries use), out_i = (c_i - NTT_i([x]_{q_i})) * q_{l-1}^-1 mod q_i,
  * i < l - 1 -- round(c / q_{l-1}) in RNS. */
-void orc_rescale(const orc_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+int orc_rescale(const orc_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t lvl) {
+  const int rc = level_ok(c, lvl, 1);
+  if (rc) return rc;
+  if (lvl < 2) return ORC_ERR_INVALID;
   const size_t N = c->n, Li = lvl, Lo = lvl - 1;
   const uint64_t ql = c->m[Lo].q, half = ql >> 1;
 #pragma omp parallel for schedule(dynamic, 1) if (n_ct > 1)
@@ -1017,6 +1052,7 @@ void orc_rescale(const orc_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n
     }
     free(x); free(y);
   }
+  return 0;
 }
 
 /* -------------------------------------------------------------- sampling */

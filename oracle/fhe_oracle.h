@@ -39,6 +39,10 @@ extern "C" {
 
 #define ORC_SCHEME_CKKS 0u
 #define ORC_SCHEME_BFV 1u
+/* refusals of the level entries (the checker does not compute what it does not
+ * implement: BFV has no reduced levels, rescale and linear transforms are CKKS) */
+#define ORC_ERR_INVALID (-1)
+#define ORC_ERR_UNSUPPORTED (-4)
 
 typedef struct orc_ctx orc_ctx;
 
@@ -95,26 +99,28 @@ uint32_t orc_galois_elt(const orc_ctx *c, int32_t steps);
  * gks [n_rot][dnum][2][L+K][N]; KS over sigma_g(ModUp(c1)) (one ModUp for all) */
 void orc_rotate_hoisted(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                         const uint64_t *gks, uint64_t *outs, uint32_t n_ct);
-void orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+int orc_rotate_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                            const uint64_t *gks, uint64_t *outs, uint32_t n_ct, uint32_t lvl);
 /* double-hoisted rotation sum: out [n_ct][2][lvl][N] = sum_r rot_{g_r}(ct), one ModDown */
-void orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+int orc_rotate_sum_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                                const uint64_t *gks, uint64_t *out, uint32_t n_ct, uint32_t lvl);
 /* hoisted linear transform (CKKS): out = sum_r pts[r] (.) rot_{g_r}(ct), one ModDown */
-void orc_linear_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
+int orc_linear_hoisted_at(const orc_ctx *c, const uint64_t *ct, uint32_t n_rot, const uint32_t *galois,
                            const uint64_t *gks, const uint64_t *pts, uint64_t *out, uint32_t n_ct, uint32_t lvl);
 
 /* ---- CKKS levels: ciphertexts [n_ct][2][lvl][N] with the first lvl Q primes
- * (1 <= lvl <= L).  Key switching at level lvl uses the full-level key's rows
+ * (1 <= lvl <= L).  The *_at entries and rescale return 0, or ORC_ERR_* for a
+ * level outside [1, L] or a BFV context below L (rescale and the linear
+ * transform: any BFV context); BFV at level L runs the BFV op.  Key switching at level lvl uses the full-level key's rows
  * of Q_lvl u P (digits partition the lvl limbs by alpha). */
-void orc_keyswitch_at(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
+int orc_keyswitch_at(const orc_ctx *c, const uint64_t *d, const uint64_t *ksk, uint64_t *out, uint32_t n,
                       uint32_t lvl);
-void orc_mul_relin_at(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
+int orc_mul_relin_at(const orc_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *rlk,
                       uint64_t *out, uint32_t n_ct, uint32_t lvl);
-void orc_rotate_at(const orc_ctx *c, const uint64_t *ct, uint32_t galois, const uint64_t *gk,
+int orc_rotate_at(const orc_ctx *c, const uint64_t *ct, uint32_t galois, const uint64_t *gk,
                    uint64_t *out, uint32_t n_ct, uint32_t lvl);
 /* rescale level lvl -> lvl - 1 (lvl >= 2): out [n_ct][2][lvl-1][N] = round(ct / q_{lvl-1}) */
-void orc_rescale(const orc_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t lvl);
+int orc_rescale(const orc_ctx *c, const uint64_t *ct, uint64_t *out, uint32_t n_ct, uint32_t lvl);
 
 /* ---- test helpers: sampling, keys, encryption */
 void orc_fill_uniform(const orc_ctx *c, uint64_t *data, uint32_t n_polys, uint32_t mod_begin,

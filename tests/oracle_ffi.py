@@ -25,6 +25,15 @@ _u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
 _lib = None
 
 
+class OracleUnsupported(ValueError):
+    """The oracle refused an op it does not implement (ORC_ERR_*), as the GPU ABI does."""
+
+
+def _ck(rc: int) -> None:
+    if rc != 0:
+        raise OracleUnsupported(f"oracle refused the call: {'ORC_ERR_UNSUPPORTED' if rc == -4 else 'ORC_ERR_INVALID' if rc == -1 else rc}")
+
+
 def build_oracle() -> str:
     src = os.path.join(ORACLE_DIR, "fhe_oracle.c")
     if (not os.path.exists(LIB_PATH)) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
@@ -60,14 +69,14 @@ def lib():
         "orc_mul_relin": (None, [vp, _u64p, _u64p, _u64p, _u64p, u32]),
         "orc_rotate": (None, [vp, _u64p, u32, _u64p, _u64p, u32]),
         "orc_galois_elt": (u32, [vp, i32]),
-        "orc_keyswitch_at": (None, [vp, _u64p, _u64p, _u64p, u32, u32]),
-        "orc_mul_relin_at": (None, [vp, _u64p, _u64p, _u64p, _u64p, u32, u32]),
-        "orc_rotate_at": (None, [vp, _u64p, u32, _u64p, _u64p, u32, u32]),
-        "orc_rescale": (None, [vp, _u64p, _u64p, u32, u32]),
+        "orc_keyswitch_at": (C.c_int, [vp, _u64p, _u64p, _u64p, u32, u32]),
+        "orc_mul_relin_at": (C.c_int, [vp, _u64p, _u64p, _u64p, _u64p, u32, u32]),
+        "orc_rotate_at": (C.c_int, [vp, _u64p, u32, _u64p, _u64p, u32, u32]),
+        "orc_rescale": (C.c_int, [vp, _u64p, _u64p, u32, u32]),
         "orc_rotate_hoisted": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32]),
-        "orc_rotate_hoisted_at": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32, u32]),
-        "orc_rotate_sum_hoisted_at": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32, u32]),
-        "orc_linear_hoisted_at": (None, [vp, _u64p, u32, _u32p, _u64p, _u64p, _u64p, u32, u32]),
+        "orc_rotate_hoisted_at": (C.c_int, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32, u32]),
+        "orc_rotate_sum_hoisted_at": (C.c_int, [vp, _u64p, u32, _u32p, _u64p, _u64p, u32, u32]),
+        "orc_linear_hoisted_at": (C.c_int, [vp, _u64p, u32, _u32p, _u64p, _u64p, _u64p, u32, u32]),
         "orc_fill_uniform": (None, [vp, _u64p, u32, u32, u32, u64]),
         "orc_sample_ternary": (None, [vp, u64, _i64p]),
         "orc_sample_cbd": (None, [vp, u64, _i64p]),
@@ -154,18 +163,18 @@ class Oracle:
     # ---- CKKS levels: ciphertexts [n][2][lvl][N] over the first lvl Q primes
     def mul_relin_at(self, a, b, rlk, lvl):
         out = np.zeros_like(a)
-        self.lib.orc_mul_relin_at(self.h, np.ascontiguousarray(a), np.ascontiguousarray(b),
-                                  np.ascontiguousarray(rlk), out, a.shape[0], lvl)
+        _ck(self.lib.orc_mul_relin_at(self.h, np.ascontiguousarray(a), np.ascontiguousarray(b),
+                                  np.ascontiguousarray(rlk), out, a.shape[0], lvl))
         return out
 
     def rotate_at(self, ct, g, gk, lvl):
         out = np.zeros_like(ct)
-        self.lib.orc_rotate_at(self.h, np.ascontiguousarray(ct), g, np.ascontiguousarray(gk), out, ct.shape[0], lvl)
+        _ck(self.lib.orc_rotate_at(self.h, np.ascontiguousarray(ct), g, np.ascontiguousarray(gk), out, ct.shape[0], lvl))
         return out
 
     def keyswitch_at(self, d, ksk, lvl):
         out = np.zeros((d.shape[0], 2, lvl, self.n), dtype=np.uint64)
-        self.lib.orc_keyswitch_at(self.h, np.ascontiguousarray(d), np.ascontiguousarray(ksk), out, d.shape[0], lvl)
+        _ck(self.lib.orc_keyswitch_at(self.h, np.ascontiguousarray(d), np.ascontiguousarray(ksk), out, d.shape[0], lvl))
         return out
 
     def rotate_hoisted(self, ct, galois, gks):
@@ -181,8 +190,8 @@ class Oracle:
         ct = np.ascontiguousarray(ct)
         gs = np.ascontiguousarray(galois, dtype=np.uint32)
         out = np.zeros(ct.shape, dtype=np.uint64)
-        self.lib.orc_rotate_sum_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), out, ct.shape[0],
-                                           ct.shape[2] if lvl is None else lvl)
+        _ck(self.lib.orc_rotate_sum_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), out, ct.shape[0],
+                                           ct.shape[2] if lvl is None else lvl))
         return out
 
     def linear_hoisted(self, ct, galois, gks, pts, lvl=None):
@@ -190,8 +199,8 @@ class Oracle:
         ct = np.ascontiguousarray(ct)
         gs = np.ascontiguousarray(galois, dtype=np.uint32)
         out = np.zeros(ct.shape, dtype=np.uint64)
-        self.lib.orc_linear_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), np.ascontiguousarray(pts),
-                                       out, ct.shape[0], ct.shape[2] if lvl is None else lvl)
+        _ck(self.lib.orc_linear_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), np.ascontiguousarray(pts),
+                                       out, ct.shape[0], ct.shape[2] if lvl is None else lvl))
         return out
 
     def rotate_hoisted_at(self, ct, galois, gks, lvl):
@@ -199,12 +208,12 @@ class Oracle:
         ct = np.ascontiguousarray(ct)
         gs = np.ascontiguousarray(galois, dtype=np.uint32)
         out = np.zeros((len(gs),) + ct.shape, dtype=np.uint64)
-        self.lib.orc_rotate_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), out, ct.shape[0], lvl)
+        _ck(self.lib.orc_rotate_hoisted_at(self.h, ct, len(gs), gs, np.ascontiguousarray(gks), out, ct.shape[0], lvl))
         return out
 
     def rescale(self, ct, lvl):
         out = np.zeros((ct.shape[0], 2, lvl - 1, self.n), dtype=np.uint64)
-        self.lib.orc_rescale(self.h, np.ascontiguousarray(ct), out, ct.shape[0], lvl)
+        _ck(self.lib.orc_rescale(self.h, np.ascontiguousarray(ct), out, ct.shape[0], lvl))
         return out
 
     def ct_add(self, a, b):

@@ -12,6 +12,8 @@ import subprocess
 import pytest
 import numpy as np
 
+import herdsman_amd.backend as hb
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "plugins", "fhe_backend.h")
 
@@ -117,3 +119,26 @@ def test_binding_rejects_bad_shapes_and_devices():
     for i, f in enumerate(bad):
         with pytest.raises(hb.FheBackendError):
             f()
+
+
+def test_build_id_ties_library_to_sources(lib, tmp_path):
+    """the library carries the hash of the sources it was
+    built from; the Makefile, the library and backend.source_build_id agree,
+    and a mutated source tree makes the loader refuse the library."""
+    import shutil
+    import subprocess
+
+    made = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "herdsman_amd"), "build-id"],
+                          check=True, capture_output=True, text=True).stdout.strip()
+    assert hb.check_build_id(lib) == made == hb.source_build_id()
+    # a copy of the source tree with one kernel file changed
+    pkg = tmp_path / "herdsman_amd"
+    shutil.copytree(os.path.join(ROOT, "herdsman_amd", "csrc"), pkg / "csrc")
+    (tmp_path / "include" / "plugins").mkdir(parents=True)
+    shutil.copy(os.path.join(ROOT, "include", "plugins", "fhe_backend.h"), tmp_path / "include" / "plugins")
+    assert hb.source_build_id(str(pkg)) == made
+    with open(pkg / "csrc" / "ntt.hip", "a") as f:
+        f.write("// edited after the build\n")
+    assert hb.source_build_id(str(pkg)) != made
+    with pytest.raises(hb.FheBackendError, match="built from other sources"):
+        hb.check_build_id(lib, str(pkg))

@@ -19,12 +19,24 @@
 typedef uint64_t u64;
 typedef uint32_t u32;
 
-enum { COL8 = 0, ROW8 = 1, FLAT8 = 2, FLAT16 = 3, LINE16 = 4 };
+enum { COL8 = 0, ROW8 = 1, FLAT8 = 2, FLAT16 = 3, LINE16 = 4, COL32 = 5, COL64 = 6, COL128 = 7 };
+// COLc (round 6): the column pass's pattern with wider row
+// segments: a tile is c adjacent columns x 4096/c rows of a 256 x 256 limb, a
+// wave instruction reads 64/c rows x c words (c = 32: two 256 B segments,
+// 64: one 512 B segment, 128: half of a 1 KiB segment pair) at the 2 KiB row
+// stride.  COL8 is c = 16 (four 128 B segments).
+template <int PAT>
+constexpr u32 col_width() { return PAT == COL32 ? 32 : PAT == COL64 ? 64 : PAT == COL128 ? 128 : 16; }
 enum { COPY = 0, READ = 1, WRITE = 2, READL2 = 3 };  // READL2: the reads cycle over 64 tiles (2 MiB, L2-resident)
 
 template <int PAT>
 __device__ __forceinline__ u32 off_of(u32 tid, u32 blk, int r) {
   if (PAT == COL8) return (tid / 16 + 16 * r) * 256 + blk * 16 + tid % 16;
+  if (PAT == COL32 || PAT == COL64 || PAT == COL128) {
+    constexpr u32 C = col_width<PAT>(), G = 256 / C;  // column groups per limb
+    const u32 row0 = (blk / G) * (4096 / C);
+    return (row0 + tid / C + (256 / C) * r) * 256 + (blk % G) * C + tid % C;
+  }
   if (PAT == ROW8) return (blk * 16 + tid / 16) * 256 + tid % 16 + 16 * r;
   if (PAT == FLAT8) return blk * 4096 + tid + 256 * r;
   if (PAT == FLAT16) return blk * 4096 + 2 * (tid + 256 * r);  // word index of a 16-B pair (r < 8)
@@ -148,7 +160,7 @@ __global__ void __launch_bounds__(256) stream_k(const u64 *in, u64 *out, u32 til
   }
 }
 
-static const char *pname[] = {"col8", "row8", "flat8", "flat16", "line16"};
+static const char *pname[] = {"col8", "row8", "flat8", "flat16", "line16", "col32", "col64", "col128"};
 static const char *mname[] = {"copy", "read", "write", "readL2"};
 
 template <int PAT, int MODE, bool PIPE, bool NTL, bool NTS>
@@ -228,6 +240,17 @@ void line_sweep(u64 *a, u64 *b, u64 *sink, size_t words) {
   run<FLAT16, READL2, false, false, false>(a, b, sink, words, false, 0);
 }
 
+// column segment width: 128 B (col8) .. 1 KiB (col128)
+template <int PAT>
+void col_width_sweep(u64 *a, u64 *b, u64 *sink, size_t words) {
+  run<PAT, READ, false, true, false>(a, b, sink, words, false, 0);
+  run<PAT, WRITE, false, false, true>(a, b, sink, words, false, 0);
+  run<PAT, COPY, false, true, true>(a, b, sink, words, true, 0);
+  run<PAT, COPY, false, true, true>(a, b, sink, words, false, 0);
+  run<PAT, COPY, true, true, true>(a, b, sink, words, true, 2);
+  run<PAT, COPY, true, true, true>(a, b, sink, words, true, 4);
+}
+
 int main(int argc, char **argv) {
   const size_t words = (size_t)4608 * 65536;  // 2.25 GiB: the roofline loop's 4608 limbs
   u64 *a, *b, *sink;
@@ -240,6 +263,14 @@ int main(int argc, char **argv) {
   hipMemset(b, 2, words * 8);
   if (argc > 1 && argv[1][0] == 'r') {  // ./stream row: lane-line against lane-contiguous pairs
     line_sweep(a, b, sink, words);
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'c') {  // ./stream col: column segment width
+    col_width_sweep<COL8>(a, b, sink, words);
+    col_width_sweep<COL32>(a, b, sink, words);
+    col_width_sweep<COL64>(a, b, sink, words);
+    col_width_sweep<COL128>(a, b, sink, words);
+    col_width_sweep<ROW8>(a, b, sink, words);
     return 0;
   }
   if (argc > 1 && argv[1][0] == 'l') {  // ./stream l2
