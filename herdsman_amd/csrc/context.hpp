@@ -55,7 +55,6 @@ struct ConvTab {
 struct fhe_ctx {
   fhe_params params{};
   int device = 0;
-  u32 num_cus = 256;  // compute units of the device (persistent grids)
   hipStream_t stream = nullptr;
   hipStream_t own_stream = nullptr;  // fhe_use_own_stream
   std::string err;
@@ -82,6 +81,7 @@ struct fhe_ctx {
   // with fuse_modup also Q limbs N^-1 (Q_j/q_i)^-1 R (q_i in digit j), so the
   // INTT of the key-switch input emits ModUp's v_i (ntt_fwd_modup_launch)
   u64 *d_iscale = nullptr;     // [nmod]
+  u64 *d_iscale_t = nullptr;   // [nmod] d_iscale times R: INTT(d2) of the split tensor product (PRO_TENSOR2 forms d2 R^-1)
   bool fuse_moddown = false;
   bool fuse_modup = false;     // also alpha <= 4
   // BFV relinearisation at two-pass sizes (alpha, K, digits <= 4): ModUp in the
@@ -91,6 +91,15 @@ struct fhe_ctx {
   u64 *d_bfv_dscale = nullptr;  // [L] (Q_j/q_i)^-1 R: the floor writes ModUp's scaled sources
   u64 *d_bfv_kscale = nullptr;  // [nmod] INTT(acc) output constants: N^-1 (Q), N^-1 (P/p_k)^-1 (P), Montgomery
   std::vector<ConvTab> modup_tabs;  // host copies of d_modup (device pointers inside)
+  // the fused key switch (ntt_ksf.hip) accumulates at the scale R^-2, which
+  // saves the own digit's R^3 product: ModUp's Q targets come out times R^-1
+  // (its P targets times R, as modup_tabs), ModDown's times R^-2, and the
+  // finish multiplies by P^-1 R^3; the own digit's base takes P and P R^-1
+  std::vector<ConvTab> modup_tabs_ksf;
+  ConvTab moddown_ksf{};
+  u64 *d_pinv3 = nullptr;  // [L] P^-1 R^3 mod q_i
+  u64 *d_pplain = nullptr; // [L] P mod q_i
+  u64 *d_pm1 = nullptr;    // [L] P R^-1 mod q_i
   std::vector<void *> blobs;   // device allocations owned by the context
   void *behz = nullptr;        // BEHZ device constants (BFV)
   void *hps = nullptr;         // HPS device constants (BFV with FHE_FLAG_BFV_HPS): BFV mul uses HPS
@@ -165,8 +174,11 @@ int fhe_fail(fhe_ctx *c, int code, const std::string &msg);
 int fhe_check(fhe_ctx *c, hipError_t e, const char *what);
 void *ctx_upload(fhe_ctx *c, const void *host, size_t bytes);  // owned blob
 int ctx_workspace(fhe_ctx *c, size_t bytes, void **out);
+// r_exp_q: the exponent for targets among the Q limbs (index < L) instead
+// (kNoExp: r_exp for every target); negative exponents scale by R^-1
+constexpr int kNoExp = 1000;
 ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst, int r_exp,
-                      bool fold_ninv = false);
+                      bool fold_ninv = false, int r_exp_q = kNoExp);
 // host modular helpers
 u64 host_mulmod(u64 a, u64 b, u64 q);
 u64 host_inv(u64 a, u64 q);

@@ -135,7 +135,7 @@ int ctx_workspace(fhe_ctx *c, size_t bytes, void **out) {
 // fold_ninv: the sources arrive as N * x (an inverse NTT without its N^-1), so
 // the per-source constant also carries N^-1
 ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector<u32> &dst, int r_exp,
-                      bool fold_ninv) {
+                      bool fold_ninv, int r_exp_q) {
   ConvTab t{};
   t.ns = (u32)src.size();
   t.nd = (u32)dst.size();
@@ -152,7 +152,9 @@ ConvTab make_conv_tab(fhe_ctx *c, const std::vector<u32> &src, const std::vector
       u64 p2 = 1;
       for (u32 k = 0; k < t.ns; ++k)
         if (k != i) p2 = hmul(p2, c->moduli[src[k]] % dm, dm);
-      for (int e = 0; e < r_exp; ++e) p2 = tomont(p2, dm);
+      const int ex = r_exp_q != kNoExp && dst[m] < c->L ? r_exp_q : r_exp;
+      for (int e = 0; e < ex; ++e) p2 = tomont(p2, dm);
+      for (int e = ex; e < 0; ++e) p2 = hmul(p2, hinv(tomont(1, dm), dm), dm);  // times R^-1
       h[(size_t)i * t.nd + m] = p2;
     }
   }
@@ -313,7 +315,40 @@ static int ctx_build(fhe_ctx *c, const fhe_params *p, u32 alpha = 0) {
         isc[i] = tomont(hmul(hinv(prod, qi), hinv((u64)c->n % qi, qi), qi), qi);
       }
       c->d_iscale = (u64 *)ctx_upload(c, isc.data(), sizeof(u64) * isc.size());
-      if (!c->d_iscale) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
+      std::vector<u64> isct(isc.size());
+      for (u32 m = 0; m < c->nmod; ++m) isct[m] = tomont(isc[m], c->moduli[m]);
+      c->d_iscale_t = (u64 *)ctx_upload(c, isct.data(), sizeof(u64) * isct.size());
+      if (!c->d_iscale || !c->d_iscale_t) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
+    }
+    // the fused key switch's tables (ntt_ksf.hip: accumulator scale R^-2)
+    if (c->fuse_modup) {
+      for (u32 j = 0; j * c->alpha < L; ++j) {
+        const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
+        std::vector<u32> src, dst;
+        for (u32 i = lo; i < hi; ++i) src.push_back(i);
+        for (u32 i = 0; i < QP; ++i)
+          if (i < lo || i >= hi) dst.push_back(i);
+        c->modup_tabs_ksf.push_back(make_conv_tab(c, src, dst, 2, c->fold_ninv, 0));  // Q targets times R^-1
+        if (!c->modup_tabs_ksf.back().h) return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
+      }
+      std::vector<u32> src, dst;
+      for (u32 k = 0; k < c->K; ++k) src.push_back(L + k);
+      for (u32 i = 0; i < L; ++i) dst.push_back(i);
+      c->moddown_ksf = make_conv_tab(c, src, dst, -1, c->fold_ninv);  // conv times R^-2
+      std::vector<u64> pinv3(L), pplain(L), pm1(L);
+      for (u32 i = 0; i < L; ++i) {
+        const u64 q = c->moduli[i];
+        u64 P = 1;
+        for (u32 k = 0; k < c->K; ++k) P = hmul(P, c->moduli[L + k] % q, q);
+        pinv3[i] = tomont(tomont(tomont(hinv(P, q), q), q), q);
+        pplain[i] = P;
+        pm1[i] = hmul(P, hinv(tomont(1, q), q), q);
+      }
+      c->d_pinv3 = (u64 *)ctx_upload(c, pinv3.data(), sizeof(u64) * L);
+      c->d_pplain = (u64 *)ctx_upload(c, pplain.data(), sizeof(u64) * L);
+      c->d_pm1 = (u64 *)ctx_upload(c, pm1.data(), sizeof(u64) * L);
+      if (!c->moddown_ksf.h || !c->d_pinv3 || !c->d_pplain || !c->d_pm1)
+        return fhe_fail(c, FHE_ERR_OOM, "ks table upload");
     }
     // BFV relinearisation with the fused passes (bfv_ks_fused, rns.hip)
     const u32 ndig = (L + c->alpha - 1) / c->alpha;
@@ -428,9 +463,6 @@ int fhe_ctx_create(const fhe_params *params, int device, fhe_ctx **out) {
   fhe_ctx *c = new (std::nothrow) fhe_ctx();
   if (!c) return FHE_ERR_OOM;
   c->device = device;
-  int ncu = 0;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
-    c->num_cus = (u32)ncu;
   int rc = ctx_build(c, params);
   if (rc) {
     g_create_error = c->err;

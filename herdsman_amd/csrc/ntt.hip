@@ -57,9 +57,11 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
   a.scale = inverse ? scale : nullptr;
   a.lazy_out = !inverse && lazy_out;
   a.src = src;
-  // N = 2^14: two passes of 7 stages with 32 sub-transforms per workgroup (35 KiB
-  // of LDS, 4 workgroups per CU) instead of one pass per residue (128 KiB,
-  // one workgroup of 16 waves per CU)
+  // N = 2^14 on special moduli: the persistent one-pass kernel (ntt_persist: one
+  // 1024-thread workgroup per CU with 128 KiB of LDS, PERSIST_K residues per
+  // workgroup, the next residue prefetched into registers).  Generic moduli and
+  // launches mixing both lazy-schedule classes take two passes of 7 stages with
+  // 32 sub-transforms per workgroup (35 KiB of LDS, 4 workgroups per CU).
   int rc;
   if (c->log_n >= NTT_PERSIST && c->log_n <= 14) {
     rc = c->log_n == 14 ? persist<14>(c, a, inverse, n_jobs)

@@ -838,7 +838,9 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
             mac128(sm, a1, b0);
             o1[h] = reduce128<SP>(sm, mi);
           }
-          const u64 t = mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi);  // d2 in [0, 2q)
+          // PRO_TENSOR2: d2 R^-1 (< 1.5q; the INTT's output scale carries the R,
+          // ntt_inv_tensor_launch); PRO_TENSOR: d2 in [0, 2q)
+          const u64 t = ALL ? mont_mul<SP>(mont_reduce<SP>(mul128(a1, b1), mi), mi.r2, mi) : mont_mul<SP>(a1, b1, mi);
           x[st * ST + h] = csub(t, mi.q);
           if constexpr (ALL) oe[h] = csub(mont_mul<SP>(t, mi.r2, mi), mi.q);  // d2 R
         }

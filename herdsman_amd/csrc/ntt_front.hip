@@ -32,7 +32,11 @@ int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 
     t.t_ndig = ndig;
     // dc feeds ModUp only: its per-source constants (N^-1 folded in) ride on
     // this INTT when ModUp is fused into the next NTT, else N^-1 is skipped
-    if (c->fuse_modup) t.scale = c->d_iscale;
+    // PRO_TENSOR2 forms d2 R^-1 (one Montgomery product): its scale carries R
+    // (d_iscale_t; without the fused ModUp, R in place of the skipped N^-1)
+    if (d2_only && !c->fold_ninv) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "split tensor product: scaling");
+    if (c->fuse_modup) t.scale = d2_only ? c->d_iscale_t : c->d_iscale;
+    else if (d2_only) t.scale = c->d_r2;
     else t.noscale = c->fold_ninv;
     const u32 n_jobs = np * L;
     int rc;

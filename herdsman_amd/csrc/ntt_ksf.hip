@@ -7,9 +7,9 @@
 // and writes ext, and EPI_KSQT reads ext back, once per output poly b.  Here
 // ONE workgroup per (limb, ciphertext, row block) does all of it for both b:
 //   1. the own digit and the base, from the ciphertexts a, b (as EPI_KSQT):
-//        acc_b = (d2 R) ksk_own,b R^-1 + base_b P      (base_0 = a0 b0, base_1 = a0 b1 + a1 b0)
+//        acc_b = d2 ksk_own,b + base_b P      (base_0 = a0 b0, base_1 = a0 b1 + a1 b0)
 //   2. every non-own digit j: the row transform of its ModUp intermediate
-//      (the forward row pass, in registers), then acc_b += ext_j ksk_j,b R^-1
+//      (the forward row pass, in registers), then acc_b += ext_j ksk_j,b
 //   3. for b = 0, 1: the row transform of NTT(conv_b)'s intermediate and the
 //      ModDown finish out_b = (acc_b - conv_b) P^-1 = base_b + (acc_b' - conv_b) P^-1
 // so ext's Q limbs are never stored (the P limbs: ksp_fused_pass below; with
@@ -20,7 +20,13 @@
 // and the base sigma_g(c0) (poly 0) gathered from the ciphertext, so
 // PRO_AUTOMORPH stores neither.
 // Bit-exact with the unfused path: the same butterflies (run_group) on the
-// same lazy ranges, every sum reduced mod q_i (acc is canonical before the finish).
+// same lazy ranges; the sums differ only in their representatives mod q_i.
+// Round 6: the accumulators run at the scale R^-2 (ModUp's Q targets arrive
+// times R^-1, ModDown's conv times R^-2, the finish multiplies by P^-1 R^3:
+// fhe_ctx::modup_tabs_ksf / moddown_ksf / d_pinv3), so the own digit is four
+// plain Montgomery products (no 128-bit product, no reduction with carry
+// compares, no R^3 product), and on moduli below 2^60 the digit sums stay lazy
+// (below 8q) until the finish: -17% VALU instructions (tools/isa_count.py).
 #include "ntt_core.hpp"
 
 #ifndef KSF_FUSE
@@ -67,8 +73,9 @@ struct KsfArgs {
   u64 *out;             // [n][2][L][N]
   const ModInfo *mods;  // the Q limbs first
   const u64 *tw;        // forward twiddles [nmod][N]
-  const u64 *pinv;      // [L] P^-1 R
-  const u64 *pr2;       // [L] P R^2
+  const u64 *pinv;      // [L] P^-1 R^3 (the accumulator scale R^-2)
+  const u64 *pplain;    // [L] P mod q_i
+  const u64 *pm1;       // [L] P R^-1 mod q_i
   u32 L, QP, kQP, ndig, alpha;
   u32 g;                // ROT: the Galois element (ta = the ciphertexts, read through sigma_g)
 };
@@ -147,11 +154,12 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  // 1. the own digit (d2 R from a1 b1) and the base times P, canonical sums below 2q
+  // 1. the own digit and the base, every term at the accumulator scale R^-2
+  //    (the finish's constant P^-1 R^3 cancels it): no 128-bit products
   u64 acc0[R], acc1[R];
   if constexpr (ROT) {
-    const u64 pr = csub(mont_mul<SP>(a.pr2[limb], 1, mi), q);  // P R
     const u64 *k0 = kb + jown * kj, *k1 = k0 + kbs;
+    const u64 one = 1, pm = a.pm1[limb];  // P R^-1
     sfor<R / 2>([&](auto I) {
       constexpr int r = 2 * decltype(I)::value;
       const u32 kr = IO::k_reg(r);
@@ -160,14 +168,14 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
       for (int h = 0; h < 2; ++h) {
         const u32 src = aut_src<LOG_N>((vio >> 3) + kr + h, a.g);
         const u64 y0 = ld_b(a0, src), y1 = ld_b(a1, src);  // sigma_g(c0), sigma_g(c1)
-        const u64 e = mont_mul<SP>(y1, mi.r2, mi);        // sigma_g(c1) R, < 1.5q
-        acc0[r + h] = harvey_csub(mont_mul<SP>(e, K0[h], mi) + mont_mul<SP>(y0, pr, mi), nq2);
+        const u64 e = mont_mul<SP>(y1, one, mi);           // sigma_g(c1) R^-1
+        acc0[r + h] = mont_mul<SP>(e, K0[h], mi) + mont_mul<SP>(y0, pm, mi);
         acc1[r + h] = mont_mul<SP>(e, K1[h], mi);
+        if constexpr (!WIDE) acc0[r + h] = harvey_csub(acc0[r + h], nq2);
       }
     });
   } else {
-    const u64 r3 = csub(mont_mul<SP>(mi.r2, mi.r2, mi), q);  // R^3
-    const u64 pr2 = a.pr2[limb];
+    const u64 pp = a.pplain[limb];  // P mod q
     const u64 *k0 = kb + jown * kj, *k1 = k0 + kbs;
     sfor<R / 2>([&](auto I) {
       constexpr int r = 2 * decltype(I)::value;
@@ -178,13 +186,15 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const u64 x0 = A0[h], x1 = A1[h], y0 = B0[h], y1 = B1[h];
-        const u64 e = mont_mul<SP>(mont_reduce<SP>(mul128(x1, y1), mi), r3, mi);        // d2 R, < 1.5q
-        const u64 d0p = mont_mul<SP>(mont_reduce<SP>(mul128(x0, y0), mi), pr2, mi);    // base_0 P
-        U128 t1 = mul128(x0, y1);
-        mac128(t1, x1, y0);
-        const u64 d1p = mont_mul<SP>(mont_reduce<SP>(t1, mi), pr2, mi);                // base_1 P
-        acc0[r + h] = harvey_csub(mont_mul<SP>(e, K0[h], mi) + d0p, nq2);
-        acc1[r + h] = harvey_csub(mont_mul<SP>(e, K1[h], mi) + d1p, nq2);
+        const u64 t = mont_mul<SP>(x1, y1, mi);                                  // d2 R^-1
+        const u64 d0 = mont_mul<SP>(x0, y0, mi);                                 // base_0 R^-1
+        const u64 d1 = mont_mul<SP>(x0, y1, mi) + mont_mul<SP>(x1, y0, mi);      // base_1 R^-1, < 4q
+        acc0[r + h] = mont_mul<SP>(t, K0[h], mi) + mont_mul<SP>(d0, pp, mi);    // < 4q
+        acc1[r + h] = mont_mul<SP>(t, K1[h], mi) + mont_mul<SP>(d1, pp, mi);
+        if constexpr (!WIDE) {
+          acc0[r + h] = harvey_csub(acc0[r + h], nq2);
+          acc1[r + h] = harvey_csub(acc1[r + h], nq2);
+        }
       }
     });
   }
@@ -202,13 +212,18 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
       const u64x2 K0 = ld2_b(k0 + kr, vio), K1 = ld2_b(k1 + kr, vio);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        acc0[r + h] = harvey_csub(acc0[r + h] + mont_mul<SP>(x[r + h], K0[h], mi), nq2);
-        acc1[r + h] = harvey_csub(acc1[r + h] + mont_mul<SP>(x[r + h], K1[h], mi), nq2);
+        // WIDE (q < 2^60): lazy sums, below 4q + 2 x 2q = 8q < 2^63 after two non-own digits
+        acc0[r + h] = acc0[r + h] + mont_mul<SP>(x[r + h], K0[h], mi);
+        acc1[r + h] = acc1[r + h] + mont_mul<SP>(x[r + h], K1[h], mi);
+        if constexpr (!WIDE) {
+          acc0[r + h] = harvey_csub(acc0[r + h], nq2);
+          acc1[r + h] = harvey_csub(acc1[r + h], nq2);
+        }
       }
     });
   }
   // 3. NTT(conv_b)'s row transform and the ModDown finish, b = 0, 1
-  u64 cb1 = (WIDE ? 2 * q2 : q2) + 1;  // B q + 1: (acc + cb1) + ~v = acc + B q - v
+  u64 cb1 = (WIDE ? 2 * q2 : q2) + 1;  // B q + 1: (acc + cb1) + ~v = acc + B q - v (< 8q WIDE)
   asm("" : "+s"(cb1));
   const u64 pinv = a.pinv[limb];
   const auto finish = [&](const u64(&acc)[R], int b) {
@@ -224,7 +239,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const u64 v = harvey_csub(x[r + h], WIDE ? nq4 : nq2);  // below 4q (WIDE) / 2q
-        const u64 s = harvey_csub(acc[r + h], nq1);
+        const u64 s = WIDE ? harvey_csub(acc[r + h], nq4) : harvey_csub(acc[r + h], nq1);  // < 4q / < q
         o[h] = harvey_csub(mont_mul<SP>((s + cb1) + ~v, pinv, mi), nq1);
       }
       st2_e(ob + IO::k_reg(r), vio, u64x2{o[0], o[1]});
@@ -233,6 +248,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksf_pass(KsfArgs a) {
   finish(acc0, 0);
   finish(acc1, 1);
 }
+
 
 template <int LOG_N, int KD, bool WIDE, bool ROT>
 int ksf_launch(fhe_ctx *c, const KsfArgs &a, u32 n) {
@@ -308,10 +324,12 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
     for (int r = 0; r < R; ++r) x[r] = lds[l2 + IO::k_reg(r) + lds_pad(IO::k_reg(r))];
     __builtin_amdgcn_sched_barrier(0);
   };
-  // acc_P,b over every digit, kept below 2q (the products are below 1.5q)
+  // acc_P,b over every digit (the products are below 1.5q): reduced by 2q
+  // after every second digit only, so below 3.5q < 2^63 at the end (q < 2^61)
   u64 acc0[R], acc1[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc0[r] = acc1[r] = 0;
+#pragma unroll
   for (int j = 0; j < KD; ++j) {
     __builtin_amdgcn_sched_barrier(0);  // the next digit's loads stay below this digit's products
     u64 x[R];
@@ -325,8 +343,12 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
       const u64x2 K0 = ld2_b(k0 + kr, vio), K1 = ld2_b(k1 + kr, vio);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        acc0[r + h] = harvey_csub(acc0[r + h] + mont_mul<SP>(x[r + h], K0[h], mi), nq2);
-        acc1[r + h] = harvey_csub(acc1[r + h] + mont_mul<SP>(x[r + h], K1[h], mi), nq2);
+        acc0[r + h] = acc0[r + h] + mont_mul<SP>(x[r + h], K0[h], mi);
+        acc1[r + h] = acc1[r + h] + mont_mul<SP>(x[r + h], K1[h], mi);
+        if (j & 1) {  // compile-time (the digit loop is unrolled)
+          acc0[r + h] = harvey_csub(acc0[r + h], nq2);
+          acc1[r + h] = harvey_csub(acc1[r + h], nq2);
+        }
       }
     });
   }
@@ -339,7 +361,11 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
     G1::template load_tw<S0>(t, twi, row, ts);
     const u32 l2 = lds_idx<S>(w, IO::k_thr(ts));
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[l2 + IO::k_reg(r) + lds_pad(IO::k_reg(r))] = harvey_csub(acc[r], nq1);
+    for (int r = 0; r < R; ++r) {
+      // canonical: below 3.5q (odd KD) or 2q (even KD) before the reductions
+      const u64 v = KD & 1 ? harvey_csub(acc[r], nq2) : acc[r];
+      lds[l2 + IO::k_reg(r) + lds_pad(IO::k_reg(r))] = harvey_csub(v, nq1);
+    }
     __syncthreads();
     const u32 l1 = lds_idx<S>(w, G1::k_thr(ts));
 #pragma unroll
@@ -436,6 +462,7 @@ int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u
 int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, const u64 *ksk, u32 ndig,
                                const u64 *ta, const u64 *tb, u64 *out, u32 n, u32 g) {
   if (!ks_fused_finish_ok(c, ndig)) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch finish: shape");
+  if (!c->d_pinv3) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused key-switch finish: tables");
   const size_t N = c->n, L = c->L, QP = c->L + c->K;
   const u32 per = 65535u;  // gridDim.y
   for (u32 c0 = 0; c0 < n; c0 += per) {
@@ -450,8 +477,9 @@ int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, cons
     a.out = out + (size_t)c0 * 2 * L * N;
     a.mods = c->d_mods;
     a.tw = c->d_tw_fwd;
-    a.pinv = c->d_pinv;
-    a.pr2 = c->d_pr2;
+    a.pinv = c->d_pinv3;
+    a.pplain = c->d_pplain;
+    a.pm1 = c->d_pm1;
     a.L = c->L;
     a.QP = (u32)QP;
     a.kQP = ctx_key_qp(c);

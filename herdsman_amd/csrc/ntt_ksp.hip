@@ -12,7 +12,9 @@
 int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows) {
   const u32 L = c->L, QP = c->L + c->K, N = c->n;
   const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
-  const ConvTab &tab = c->modup_tabs[j];
+  // q_rows false (the fused key switch): Q targets at its accumulator scale
+  if (!q_rows && c->modup_tabs_ksf.size() <= j) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp: ksf tables");
+  const ConvTab &tab = q_rows ? c->modup_tabs[j] : c->modup_tabs_ksf[j];
   if (c->log_n <= 14 || tab.ns > 4) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp: log_n / digit size");
   const u32 per = 65535u;  // gridDim.y
   for (u32 p0 = 0; p0 < n; p0 += per) {

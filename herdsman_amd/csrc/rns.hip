@@ -1045,7 +1045,8 @@ static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, 
     else rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale);
     if (rc) return rc;
     if (tsrc && !(ksq && KSP_FUSE)) return fhe_fail(c, FHE_ERR_INVALID, "split tensor product without EPI_KSQ");
-    return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, &c->moddown, ksq ? ext : nullptr,
+    const ConvTab *md = tsrc && tsrc->fused ? &c->moddown_ksf : &c->moddown;  // the fused finish's scale
+    return ntt_fwd_combine_launch(c, conv, 2 * n, acc, QP, base, out, add_mask, md, ksq ? ext : nullptr,
                                   ksk, ndig, base_g, nullptr, nullptr, ext_g, nullptr, tsrc);
   }
   if (base_g) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "rotated key-switch base without the fused ModDown");

@@ -16,6 +16,8 @@
 #   optrace=OP     rocprofv3 --kernel-trace --stats of tools/op_bench.py OP (bfv_mul, ckks_mul, ckks_rot)
 #   prof           tools/profile_round.sh (roofline stats, PMC passes; summarise with tools/collect_profile.py)
 #   steptable      rocprofv3 kernel trace of one C5 wave loop -> tools/step_table.py
+#   valu=V1,V2     SQ_INSTS_VALU + SQ_WAVES of op_bench ckks_mul (128 per call) per variant -> tools/valu_count.py
+#   valuop=OP:V1,V2  the same for another op_bench op (bfv_mul, ckks_rot, ...)
 #   wgbench        GpuWorkerGroup MapTask throughput end to end (wg_run bench, files under /tmp on the box)
 set -e
 export TMPDIR=/tmp
@@ -53,6 +55,14 @@ for s in "$@"; do
     optrace=*) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/op_${s#optrace=}" -o run -- python3 tools/op_bench.py "${s#optrace=}" --batch 128 --reps 5 > "$O/op_${s#optrace=}.log" 2>&1 ;;
     prof) timeout -k 10 1100 bash tools/profile_round.sh "$O/prof" > "$O/prof.log" 2>&1 ;;
     wgbench) rm -rf /tmp/wgb && timeout -k 10 400 herdsman_amd/bin/wg_run bench /tmp/wgb 0,16,12,4,3,0 4 64 4 16 6 > "$O/wg_bench.log" 2>&1; rm -rf /tmp/wgb ;;
+    valu=*|valuop=*)
+      if [ "${s%%=*}" = valuop ]; then spec=${s#valuop=}; OP=${spec%%:*}; VS=${spec#*:}; else OP=ckks_mul; VS=${s#valu=}; fi
+      IFS=, read -r -a vs <<< "$VS"
+      lib_of() { if [ "$1" = main ]; then echo herdsman_amd/lib/libherdsman_fhe.so; else echo herdsman_amd/var/$1/libherdsman_fhe.so; fi; }
+      for v in "${vs[@]}"; do
+        HERD_FHE_LIB=$(lib_of $v) timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d "$O/valu_$OP/$v" -o run -- python3 tools/op_bench.py $OP --batch 128 --reps 2 > "$O/valu_$OP.$v.log" 2>&1
+      done
+      python3 tools/valu_count.py "$O/valu_$OP" "${vs[@]}" > "$O/valu_$OP.txt" 2>&1 || true ;;
     steptable) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/step" -o run -- python3 tools/op_bench.py ckks_mul --batch 128 --reps 8 > "$O/step.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
