@@ -228,7 +228,10 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
 // through d_iscale); ext_j [n][ndig*QP][N] slots outside the digit receive
 // the lazy (< 8q) NTT outputs times R
 // (q_rows false: every target keeps its column-pass output, for the fused key switch)
-int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows = true);
+// ksf_scale (q_rows false only): the Q targets at the fused CKKS finish's
+// scale (modup_tabs_ksf); else every target times R (modup_tabs; BFV)
+int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows = true,
+                         bool ksf_scale = true);
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n);
 // INTT(acc_P) with the P limbs' key-switching inner product in its first pass
 // (ext_g != 0: ext is read as sigma_g(ext), the hoisted rotation's inner product)
@@ -244,7 +247,15 @@ bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig);
 // (g != 0: the rotation's finish, ta = the ciphertexts read through sigma_g, tb unused)
 // ntt_ksp_fused_launch: the P side -- the P limbs' ModUp row transforms, their
 // inner product and INTT(acc_P) (acc's P rows as ntt_inv_ksp_launch leaves them)
-int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig);
+// (all_limbs: BFV -- every Q u P limb, each digit's column-pass intermediates
+// own limbs included, INTT output constants d_bfv_kscale)
+int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig,
+                         bool all_limbs = false);
+// the BFV key switch without a stored ext applies (ntt_ksf.hip)
+bool bfv_ks_extfree_ok(const fhe_ctx *c, u32 ndig);
+// the first (column) pass of a forward NTT alone (two-pass sizes): its
+// intermediate for a fused consumer that runs the row transforms itself
+int ntt_fwd_col_launch(fhe_ctx *c, const LimbMap &m);
 int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, const u64 *ksk, u32 ndig,
                                const u64 *ta, const u64 *tb, u64 *out, u32 n, u32 g = 0);
 // d2_only (PRO_TENSOR2, two-pass sizes): out is not written; the ModDown

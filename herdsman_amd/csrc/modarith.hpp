@@ -369,13 +369,15 @@ HD u64 dot_cols(const u64 (&v)[NS], const u32 (&h0)[NS], const u32 (&h1)[NS], co
   const u64 hi = (c1 >> 33) + (c2 >> 2) + (lo1 < c0) + (lo < lo1);
   return mont_reduce<SP>(U128{lo, hi}, m);
 }
-// The same sum for a special modulus m = mh 2^32 + 1 < 2^60 (h1 < 2^29): the
+// The same sum for a special modulus m = mh 2^32 + 1 < 2^61 where one side of
+// every product is below 2^60 (m < 2^60, or sources v < 2^60: then v1 < 2^29
+// or h1 < 2^29, and C1 stays below 2^64; result < 1.25m): the
 // reduction runs on the columns themselves, as Montgomery rounds of 31, 31
 // and 2 bits (m = 1 mod 2^31, so each quotient digit is -t mod 2^k and its
 // multiple of m is u (m >> k) 2^k + u): C0 is folded into C1's accumulator, C1
 // into C2's, with no 128-bit combine.  Each accumulator starts at 2^k - 1, so
 // its top (acc >> k) already carries the round's "+ [t != 0]" and the digit is
-// ~acc mod 2^k.  Bounds: C1 < 2^63 + 2^62 + 2^61, C2 < 2^62; result < 2q.
+// ~acc mod 2^k.  Bounds: C1 < 7 2^61 < 2^64, C2 < 2^62; result < 1.25m.
 template <int NS>
 HD u64 dot_cols_sp60(const u64 (&v)[NS], const u32 (&h0)[NS], const u32 (&h1)[NS], u32 q_hi) {
   static_assert(NS >= 1 && NS <= 4, "column sums stay below 2^64 for at most 4 terms");

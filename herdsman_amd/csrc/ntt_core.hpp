@@ -144,6 +144,9 @@ struct NttArgs {
   // where the source word exceeds c_lift_half (0: plain conversion)
   u64 c_lift_half;
   const u64 *c_lift_sub;  // [nd] q_l mod q_m
+  // every source modulus is below 2^60: the column sums reduce in place
+  // (dot_cols_sp60) for special targets below 2^61 too, not only below 2^60
+  u32 c_src60;
 };
 
 // The passes shared by several entry points, compiled once (ntt.hip, ntt_conv*.hip):
@@ -399,8 +402,11 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
           ++n;
         }
       }
-      // 64-bit adds of SGPR constants as single v_lshl_add_u64 (no carry
-      // chain through VCC, which costs s_nop wait states): a - b = a + (2q+1) + ~b - 2q
+      // 64-bit adds of SGPR constants as single v_lshl_add_u64; the butterfly's
+      // difference U + 2q - V as v_lshl_add_u64 + v_sub_co_u32 + v_subb_co_u32
+      // (round 6: 4 issue slots against 6 for (U + 2q + 1) + ~V; the borrow's
+      // VCC hazard costs s_nop wait states, which other waves fill: headline
+      // +1.4..2.0%, NTT INV -2.2% on a paired A/B, profiles/r06/ab_bfly_sub.txt)
       u64 nq2 = 0 - q2, q2p1 = q2 + 1, nq4 = 0 - 2 * q2;
       asm("" : "+s"(nq2));
       asm("" : "+s"(q2p1));
@@ -419,7 +425,7 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
             A[i] = Y;
           } else {
             U[i] = harvey_csub(X + Y, nq2);
-            A[i] = (X + q2p1) + ~Y;
+            A[i] = (X + q2) - Y;
           }
         }
         if constexpr (SP) mont_mul_sp_vec<CH>(V, A, Wt, mi.q_hi);
@@ -428,7 +434,7 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
         for (int i = 0; i < CH; ++i) {
           if (!INV) {
             x[lo_idx[c0 + i]] = U[i] + V[i];
-            x[lo_idx[c0 + i] + half] = (U[i] + q2p1) + ~V[i];
+            x[lo_idx[c0 + i] + half] = (U[i] + q2) - V[i];
           } else {
             x[lo_idx[c0 + i]] = U[i];
             x[lo_idx[c0 + i] + half] = V[i];
@@ -1011,6 +1017,10 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
       u32 hc0[NS], hc1[NS];  // the constants' 31-bit digits (uniform, SGPRs)
 #pragma unroll
       for (int i = 0; i < NS; ++i) split31(ep.h[i], hc0[i], hc1[i]);
+      // special targets: the in-place column reduction where one side of every
+      // product is below 2^60 (WIDE targets, or sources below 2^60: ModUp's P
+      // targets; result < 1.25q), else the 128-bit combine (a uniform branch)
+      const bool sp60 = CONV_COLS && SP && CONV_SP60 && (WIDE || a.c_src60);
 #pragma unroll
       for (int c0 = 0; c0 < R; c0 += 4) {
         u64 sv[4][NS];
@@ -1019,11 +1029,15 @@ __device__ __forceinline__ void pass_body(const NttArgs &a, u64 *lds, u64 *data,
 #pragma unroll
           for (int i = 0; i < NS; ++i)
             sv[j][i] = ld_b(ep.src + i * NW + ((size_t)GF::k_reg(c0 + j) << PG::LS), voff);
+        if (sp60) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          x[c0 + j] = CONV_COLS && SP && WIDE && CONV_SP60 ? dot_cols_sp60<NS>(sv[j], hc0, hc1, mi.q_hi)  // < 2q
-                      : CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                                  // < 2q
-                                  : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);                   // < 4q
+          for (int j = 0; j < 4; ++j) x[c0 + j] = dot_cols_sp60<NS>(sv[j], hc0, hc1, mi.q_hi);  // < 1.25q
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            x[c0 + j] = CONV_COLS ? dot_cols<NS, SP>(sv[j], hc0, hc1, mi)                  // < 2q
+                                  : dot_mont_lazy<NS, SP, WIDE>(sv[j], ep.h, 1, NS, mi);   // < 4q
+        }
         if constexpr (NS == 1 && CONV_COLS) {
           // rescale: the central lift (x - q_l for x > q_l / 2) of the single
           // source, as y + q - [q_l]_{q_m} < 3q (a uniform branch per launch)

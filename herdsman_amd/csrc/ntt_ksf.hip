@@ -63,6 +63,7 @@ struct KspArgs {
   const ModInfo *mods;
   const u64 *twf, *twi; // forward / inverse twiddles [nmod][N]
   u32 L, QP, kQP, kshift, ndig;
+  u32 l0;               // the launch's first limb (L: the P limbs; 0: BFV's Q limbs)
 };
 
 struct KsfArgs {
@@ -271,6 +272,9 @@ int ksf_dispatch(fhe_ctx *c, const KsfArgs &a, u32 n) {
 // (they are all non-own), forms acc_P,b = sum_j ext_j ksk_j,b R^-1 for b = 0, 1
 // and runs the first (row) pass of INTT(acc_P,b) on it, so the ModUp row pass
 // and PRO_KSP's ext reads go away; the INTT's column pass follows as before.
+// BFV (round 6, all limbs): the same over every limb of Q u P -- on a Q limb
+// the own digit's slot holds the column-pass intermediate of the limb's own
+// d R -- so BFV's ext is never written by a row pass and never read back.
 template <int LOG_N, int KD, bool WIDE, bool SP>
 __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
   constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
@@ -280,7 +284,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
   extern __shared__ u64 lds[];
   constexpr size_t N = (size_t)1 << LOG_N;
   const u32 tid = threadIdx.x;
-  u32 bx = blockIdx.x, ct = blockIdx.y, pl = blockIdx.z;  // pl: P limb (0..K-1)
+  u32 bx = blockIdx.x, ct = blockIdx.y, pl = blockIdx.z;  // pl: the launch's limb (0..gridDim.z-1)
   if (((gridDim.x * gridDim.z) & 7) == 0) {
     const u32 np = gridDim.y, lin = blockIdx.x + gridDim.x * (blockIdx.y + np * blockIdx.z);
     const u32 r = lin >> 3, g = (r / np) * 8 + (lin & 7);
@@ -288,7 +292,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
     bx = g % gridDim.x;
     pl = g / gridDim.x;
   }
-  const u32 limb = a.L + pl;  // index in Q u P
+  const u32 limb = a.l0 + pl;  // index in Q u P
   const ModInfo mi = a.mods[limb];
   const u64 q = mi.q, q2 = 2 * q;
   const u64 *twf = a.twf + ((size_t)limb << LOG_N), *twi = a.twi + ((size_t)limb << LOG_N);
@@ -296,7 +300,7 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
   const u32 row = bx * W + w, gb = row << S;
   const u32 vin = (gb + G0::k_thr(ts)) << 3;
   const u32 vio = (gb + IO::k_thr(ts)) << 3;
-  const u64 *kb = a.ksk + (size_t)(limb + a.kshift) * N;  // P limbs: key row i + kshift
+  const u64 *kb = a.ksk + (size_t)(limb + a.kshift) * N;  // key row i + kshift (a view's P limbs)
   const size_t kj = (size_t)2 * a.kQP * N, kbs = (size_t)a.kQP * N;
   const u64 *eb = a.ext + ((size_t)ct * a.ndig * a.QP + limb) * N;
   u64 nq1 = 0 - q, nq2 = 0 - q2;
@@ -390,37 +394,59 @@ __global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
 }  // namespace
 
 template <int LOG_N, int KD, bool WIDE>
-int ksp_launch(fhe_ctx *c, const KspArgs &a, u32 n) {
+int ksp_launch(fhe_ctx *c, const KspArgs &a, u32 n, u32 nl) {
   constexpr size_t lds = lds_bytes<8, 16>();
-  const dim3 grid((1u << (LOG_N - 8)) / 16, n, c->K);
+  const dim3 grid((1u << (LOG_N - 8)) / 16, n, nl);
   if (c->special) hipLaunchKernelGGL((ksp_fused_pass<LOG_N, KD, WIDE, true>), grid, dim3(256), lds, c->stream, a);
   else hipLaunchKernelGGL((ksp_fused_pass<LOG_N, KD, WIDE, false>), grid, dim3(256), lds, c->stream, a);
   return fhe_check(c, hipGetLastError(), "ksp_fused_pass launch");
 }
 template <int LOG_N, int KD>
-int ksp_dispatch(fhe_ctx *c, const KspArgs &a, u32 n) {
-  return c->moduli[c->L] < (1ull << 60) ? ksp_launch<LOG_N, KD, true>(c, a, n) : ksp_launch<LOG_N, KD, false>(c, a, n);
+int ksp_dispatch(fhe_ctx *c, const KspArgs &a, u32 n, u32 nl) {
+  return c->moduli[a.l0] < (1ull << 60) ? ksp_launch<LOG_N, KD, true>(c, a, n, nl)
+                                        : ksp_launch<LOG_N, KD, false>(c, a, n, nl);
+}
+// every modulus of [l0, l0 + nl) in one lazy-schedule class
+static bool one_class(const fhe_ctx *c, u32 l0, u32 nl) {
+  const bool wide = c->moduli[l0] < (1ull << 60);
+  for (u32 i = l0 + 1; i < l0 + nl; ++i)
+    if ((c->moduli[i] < (1ull << 60)) != wide) return false;
+  return true;
 }
 
 // The fused finish applies: N = 2^15 or 2^16 (a 256-point row pass), at most 3
 // digits, the Q limbs in one lazy-schedule class and the P limbs in one.
 bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig) {
-  if (!KSF_FUSE || (c->log_n != 15 && c->log_n != 16) || ndig < 1 || ndig > 3 || !c->L) return false;
-  const bool wide = c->moduli[0] < (1ull << 60);
-  for (u32 i = 1; i < c->L; ++i)
-    if ((c->moduli[i] < (1ull << 60)) != wide) return false;
+  if (!KSF_FUSE || (c->log_n != 15 && c->log_n != 16) || ndig < 1 || ndig > 3 || !c->L || c->K < 1) return false;
   // the P side (ntt_ksp_fused_launch): one lazy-schedule class over the P limbs too
-  const bool pwide = c->moduli[c->L] < (1ull << 60);
-  for (u32 k = 1; k < c->K; ++k)
-    if ((c->moduli[c->L + k] < (1ull << 60)) != pwide) return false;
-  return c->K >= 1;
+  return one_class(c, 0, c->L) && one_class(c, c->L, c->K);
+}
+
+#ifndef BFV_KS_EXTFREE
+#define BFV_KS_EXTFREE 1  // BFV: ModUp's row transforms inside the all-limb inner-product pass (ksp_fused_pass)
+#endif
+int ntt_fwd_col_launch(fhe_ctx *c, const LimbMap &m) {
+  if (c->log_n < 15) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "column pass alone: log_n");
+  NttArgs a{};
+  a.map = m;
+  a.tw = c->d_tw_fwd;
+  a.mods = c->d_mods;
+  a.ninv = c->d_ninv;
+  a.log_n = c->log_n;
+  return m.n_polys * m.cnt ? ntt_col_plain(c, a, false, m.n_polys * m.cnt) : FHE_OK;
+}
+
+bool bfv_ks_extfree_ok(const fhe_ctx *c, u32 ndig) {
+  return BFV_KS_EXTFREE && c->bfv_ks_fuse && c->d_bfv_kscale && !c->key_pshift && ks_fused_finish_ok(c, ndig);
 }
 
 // INTT(acc_P) with the P limbs' ModUp row transforms and inner product fused
 // into its first pass (ksp_fused_pass), then its column pass (d_iscale), as
 // ntt_inv_ksp_launch leaves acc's P rows
-int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig) {
+int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, bool all_limbs) {
   if (!ks_fused_finish_ok(c, ndig)) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused P-limb key switch: shape");
+  if (all_limbs && !bfv_ks_extfree_ok(c, ndig))
+    return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused all-limb key switch: BFV tables");
   const u32 L = c->L, K = c->K, QP = L + K;
   const size_t N = c->n;
   const u32 per = 32767u;  // ciphertexts per launch (the column pass takes 2 polys per ct on gridDim.y)
@@ -436,25 +462,30 @@ int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u
     k.L = L;
     k.QP = QP;
     k.kQP = ctx_key_qp(c);
-    k.kshift = c->key_pshift;
     k.ndig = ndig;
-    int rc;
-    if (c->log_n == 15) {
-      rc = ndig == 1 ? ksp_dispatch<15, 1>(c, k, nc) : ndig == 2 ? ksp_dispatch<15, 2>(c, k, nc)
-                                                                  : ksp_dispatch<15, 3>(c, k, nc);
-    } else {
-      rc = ndig == 1 ? ksp_dispatch<16, 1>(c, k, nc) : ndig == 2 ? ksp_dispatch<16, 2>(c, k, nc)
-                                                                  : ksp_dispatch<16, 3>(c, k, nc);
+    int rc = FHE_OK;
+    // one launch per modulus class: BFV's Q limbs (key rows = limb), then the P limbs
+    for (int part = all_limbs ? 0 : 1; part < 2 && !rc; ++part) {
+      k.l0 = part ? L : 0;
+      k.kshift = part ? c->key_pshift : 0;
+      const u32 nl = part ? K : L;
+      if (c->log_n == 15) {
+        rc = ndig == 1 ? ksp_dispatch<15, 1>(c, k, nc, nl) : ndig == 2 ? ksp_dispatch<15, 2>(c, k, nc, nl)
+                                                                        : ksp_dispatch<15, 3>(c, k, nc, nl);
+      } else {
+        rc = ndig == 1 ? ksp_dispatch<16, 1>(c, k, nc, nl) : ndig == 2 ? ksp_dispatch<16, 2>(c, k, nc, nl)
+                                                                        : ksp_dispatch<16, 3>(c, k, nc, nl);
+      }
     }
     if (rc) return rc;
     NttArgs a{};
-    a.map = LimbMap{k.acc, QP, K, L, QP, 0, 0, 2 * nc};
+    a.map = all_limbs ? LimbMap{k.acc, QP, QP, 0, QP, 0, 0, 2 * nc} : LimbMap{k.acc, QP, K, L, QP, 0, 0, 2 * nc};
     a.tw = c->d_tw_inv;
     a.mods = c->d_mods;
     a.ninv = c->d_ninv;
     a.log_n = c->log_n;
-    a.scale = c->d_iscale;
-    if ((rc = ntt_col_plain(c, a, true, 2 * nc * K))) return rc;
+    a.scale = all_limbs ? c->d_bfv_kscale : c->d_iscale;
+    if ((rc = ntt_col_plain(c, a, true, 2 * nc * a.map.cnt))) return rc;
   }
   return FHE_OK;
 }

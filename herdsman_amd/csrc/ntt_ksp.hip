@@ -9,12 +9,13 @@
 // INTT through d_iscale) as its prologue (PRO_CONV), so the converted limbs
 // never make an HBM round trip; the row pass leaves lazy outputs (< 8q) for
 // the inner product on special moduli, as keyswitch_run's separate NTT does.
-int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows) {
+int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows, bool ksf_scale) {
   const u32 L = c->L, QP = c->L + c->K, N = c->n;
   const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
   // q_rows false (the fused key switch): Q targets at its accumulator scale
-  if (!q_rows && c->modup_tabs_ksf.size() <= j) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp: ksf tables");
-  const ConvTab &tab = q_rows ? c->modup_tabs[j] : c->modup_tabs_ksf[j];
+  const bool ksf = !q_rows && ksf_scale;
+  if (ksf && c->modup_tabs_ksf.size() <= j) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp: ksf tables");
+  const ConvTab &tab = ksf ? c->modup_tabs_ksf[j] : c->modup_tabs[j];
   if (c->log_n <= 14 || tab.ns > 4) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp: log_n / digit size");
   const u32 per = 65535u;  // gridDim.y
   for (u32 p0 = 0; p0 < n; p0 += per) {
@@ -32,6 +33,8 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
     a.c_ns = tab.ns;
     a.c_nd = tab.nd;
     a.c_h = tab.h;
+    a.c_src60 = 1;
+    for (u32 i = lo; i < hi; ++i) a.c_src60 &= c->moduli[i] < (1ull << 60);
     const u32 n_jobs = np * a.map.cnt;
     // one launch per modulus class where that splits the targets into a Q part
     // and a P part of one class each (ntt_pass WM: a kernel carrying both lazy

@@ -1107,28 +1107,39 @@ static int bfv_moddown_impl(fhe_ctx *c, const u64 *acc, const u64 *base, u64 *ou
 // Split for hoisted rotations: bfv_ks_extend once per input, bfv_ks_finish per
 // key (ext_g: the inner product reads sigma_g(ext), PRO_KSPG; base_ginv: the
 // base is read as sigma_g(base) by the coefficient map, base apart from out).
+// extfree (round 6, bfv_ks_extfree_ok): ext keeps every digit's COLUMN-pass
+// intermediates (ModUp's targets and the own limbs' column pass), and the
+// all-limb fused pass (ksp_fused_pass) row-transforms them itself: ext is never
+// written by a row pass and never read back.  Hoisted rotations gather ext
+// through sigma_g and keep the stored, row-transformed ext.
 static bool bfv_fused(const fhe_ctx *c) { return c->bfv_ks_fuse && BFV_KS_FUSE; }
-static int bfv_ks_extend(fhe_ctx *c, const KsWs &w, u32 n) {
+static int bfv_ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool extfree = false) {
   const u32 L = c->L, QP = L + c->K, N = c->n, ndig = w.ndig;
   int rc;
   for (u32 j = 0; j < ndig; ++j)
-    if ((rc = ntt_fwd_modup_launch(c, w.dc, w.ext, n, ndig, j))) return rc;
+    if ((rc = ntt_fwd_modup_launch(c, w.dc, w.ext, n, ndig, j, !extfree, false))) return rc;
   for (u32 j = 0; j < ndig; ++j) {
     const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
-    if ((rc = ntt_launch(c, LimbMap{w.ext + (size_t)j * QP * N, ndig * QP, hi - lo, lo, hi - lo, 0, 0, n}, false,
-                         false, c->special)))
+    const LimbMap own{w.ext + (size_t)j * QP * N, ndig * QP, hi - lo, lo, hi - lo, 0, 0, n};
+    if (extfree) {
+      if ((rc = ntt_fwd_col_launch(c, own))) return rc;
+    } else if ((rc = ntt_launch(c, own, false, false, c->special))) {
       return rc;
+    }
   }
   return FHE_OK;
 }
 static int bfv_ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
-                         u32 ext_g = 0, u32 base_ginv = 0) {
-  int rc = ntt_inv_ksp_launch(c, w.acc, w.ext, ksk, n, w.ndig, ext_g, true);
+                         u32 ext_g = 0, u32 base_ginv = 0, bool extfree = false) {
+  int rc = extfree ? ntt_ksp_fused_launch(c, w.acc, w.ext, ksk, n, w.ndig, true)
+                   : ntt_inv_ksp_launch(c, w.acc, w.ext, ksk, n, w.ndig, ext_g, true);
   return rc ? rc : SP_DISPATCH(c, bfv_moddown_impl, c, w.acc, base, out, n, add_mask, base_ginv);
 }
-static int bfv_ks_fused(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask) {
-  int rc = bfv_ks_extend(c, w, n);
-  return rc ? rc : bfv_ks_finish(c, w, ksk, base, out, n, add_mask);
+static int bfv_ks_fused(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
+                        u32 base_ginv = 0) {
+  const bool ef = bfv_ks_extfree_ok(c, w.ndig);
+  int rc = bfv_ks_extend(c, w, n, ef);
+  return rc ? rc : bfv_ks_finish(c, w, ksk, base, out, n, add_mask, 0, base_ginv, ef);
 }
 
 // Hybrid key switching of an arbitrary input d ([n][d_stride limbs], the L
@@ -1201,8 +1212,7 @@ int rotate_impl(fhe_ctx *c, const u64 *ct, u32 g, const u64 *gk, u64 *out, u32 n
     if ((rc = SP_DISPATCH(c, automorph_ks_impl, c, ct, apart ? nullptr : base, w.dc, w.ext, g, n, w.ndig, false,
                           c->d_bfv_dscale)))
       return rc;
-    if ((rc = bfv_ks_extend(c, w, n))) return rc;
-    return bfv_ks_finish(c, w, gk, apart ? ct : base, out, n, 1u, 0, apart ? galois_inv(g, c->log_n) : 0);
+    return bfv_ks_fused(c, w, gk, apart ? ct : base, out, n, 1u, apart ? galois_inv(g, c->log_n) : 0);
   }
   if ((rc = SP_DISPATCH(c, automorph_ks_impl, c, ct, base, w.dc, w.ext, g, n, w.ndig, ntt_form, nullptr))) return rc;
   return keyswitch_run(c, w, gk, base, out, n, 1u, ntt_form);

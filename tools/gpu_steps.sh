@@ -18,6 +18,7 @@
 #   steptable      rocprofv3 kernel trace of one C5 wave loop -> tools/step_table.py
 #   valu=V1,V2     SQ_INSTS_VALU + SQ_WAVES of op_bench ckks_mul (128 per call) per variant -> tools/valu_count.py
 #   valuop=OP:V1,V2  the same for another op_bench op (bfv_mul, ckks_rot, ...)
+#   abop=OP:V1,V2  op_bench OP (128 per call, 20 reps) per variant, 3 interleaved reps ("OP+f": --openfhe-primes)
 #   wgbench        GpuWorkerGroup MapTask throughput end to end (wg_run bench, files under /tmp on the box)
 set -e
 export TMPDIR=/tmp
@@ -63,6 +64,13 @@ for s in "$@"; do
         HERD_FHE_LIB=$(lib_of $v) timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d "$O/valu_$OP/$v" -o run -- python3 tools/op_bench.py $OP --batch 128 --reps 2 > "$O/valu_$OP.$v.log" 2>&1
       done
       python3 tools/valu_count.py "$O/valu_$OP" "${vs[@]}" > "$O/valu_$OP.txt" 2>&1 || true ;;
+    abop=*)
+      spec=${s#abop=}; OP=${spec%%:*}; IFS=, read -r -a vs <<< "${spec#*:}"
+      FL=""; case $OP in *+f) OP=${OP%+f}; FL=--openfhe-primes;; esac
+      lib_of() { if [ "$1" = main ]; then echo herdsman_amd/lib/libherdsman_fhe.so; else echo herdsman_amd/var/$1/libherdsman_fhe.so; fi; }
+      for rep in 1 2 3; do for v in "${vs[@]}"; do
+        echo "$v rep$rep $(HERD_FHE_LIB=$(lib_of $v) timeout -k 10 200 python3 tools/op_bench.py $OP $FL --batch 128 --reps 20 2>/dev/null | tail -n 1)"
+      done; done > "$O/abop_$OP${FL:+_f}.txt" ;;
     steptable) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/step" -o run -- python3 tools/op_bench.py ckks_mul --batch 128 --reps 8 > "$O/step.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
