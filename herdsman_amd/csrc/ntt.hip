@@ -14,19 +14,22 @@ int ntt_row_plain(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) { return r
 #endif
 
 // the persistent one-residue-per-workgroup pass (ntt_persist), or 1 if the
-// launch's moduli mix both lazy-schedule classes (the two-pass path takes it)
-// Special moduli only: generic moduli keep the two-pass path, because ROCm
-// 7.2's backend fails some generic instantiations of the multi-residue kernel
-// ("illegal VGPR to SGPR copy": the inverse, the narrow forward schedule).
-template <int LOG_N>
-static int persist(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
-  if (!c->special) return 1;
-  if (inv) return launch_persist<LOG_N, true, true, 0>(c, a, n_jobs);
+// launch's moduli mix both lazy-schedule classes (the two-pass path takes it).
+// Generic moduli too (round 6): the modulus constants the butterflies pin in
+// SGPRs are made visibly uniform (uniform64), which clears ROCm 7.2's
+// "illegal VGPR to SGPR copy" on the generic multi-residue instantiations.
+template <int LOG_N, bool SP>
+static int persist_sp(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  if (inv) return launch_persist<LOG_N, true, SP, 0>(c, a, n_jobs);
   switch (wide_mode(c, a.map)) {
-    case 1: return launch_persist<LOG_N, false, true, 1>(c, a, n_jobs);
-    case 0: return launch_persist<LOG_N, false, true, 0>(c, a, n_jobs);
+    case 1: return launch_persist<LOG_N, false, SP, 1>(c, a, n_jobs);
+    case 0: return launch_persist<LOG_N, false, SP, 0>(c, a, n_jobs);
   }
   return 1;
+}
+template <int LOG_N>
+static int persist(fhe_ctx *c, const NttArgs &a, bool inv, u32 n_jobs) {
+  return c->special ? persist_sp<LOG_N, true>(c, a, inv, n_jobs) : persist_sp<LOG_N, false>(c, a, inv, n_jobs);
 }
 
 int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool lazy_out, const u64 *scale,
@@ -57,11 +60,11 @@ int ntt_launch(fhe_ctx *c, const LimbMap &m, bool inverse, bool noscale, bool la
   a.scale = inverse ? scale : nullptr;
   a.lazy_out = !inverse && lazy_out;
   a.src = src;
-  // N = 2^14 on special moduli: the persistent one-pass kernel (ntt_persist: one
-  // 1024-thread workgroup per CU with 128 KiB of LDS, PERSIST_K residues per
-  // workgroup, the next residue prefetched into registers).  Generic moduli and
-  // launches mixing both lazy-schedule classes take two passes of 7 stages with
-  // 32 sub-transforms per workgroup (35 KiB of LDS, 4 workgroups per CU).
+  // N = 2^14: the persistent one-pass kernel (ntt_persist: one 1024-thread
+  // workgroup per CU with 128 KiB of LDS, PERSIST_K residues per workgroup, the
+  // next residue prefetched into registers).  Launches mixing both lazy-schedule
+  // classes take two passes of 7 stages with 32 sub-transforms per workgroup
+  // (35 KiB of LDS, 4 workgroups per CU).
   int rc;
   if (c->log_n >= NTT_PERSIST && c->log_n <= 14) {
     rc = c->log_n == 14 ? persist<14>(c, a, inverse, n_jobs)

@@ -354,6 +354,16 @@ struct IoL {
   }
 };
 
+// a wave-uniform 64-bit value made visibly uniform (two v_readfirstlane_b32, or
+// s_movs when it already lives in SGPRs), so an asm "+s" constraint can pin it
+// in SGPRs: without it ROCm 7.2 fails the generic-moduli persistent pass, whose
+// unrolled residue loop carries the modulus through a VGPR phi ("illegal VGPR
+// to SGPR copy")
+__device__ __forceinline__ u64 uniform64(u64 x) {
+  const u32 lo = __builtin_amdgcn_readfirstlane((u32)x), hi = __builtin_amdgcn_readfirstlane((u32)(x >> 32));
+  return ((u64)hi << 32) | lo;
+}
+
 // x - m if that is non-negative, else x (x, m < 2^63; neg_m = -m), selected
 // by the sign word with two v_bfi_b32: no VCC compare/select, so no hazard nops
 __device__ __forceinline__ u64 harvey_csub(u64 x, u64 neg_m) {
@@ -407,9 +417,10 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
       // (round 6: 4 issue slots against 6 for (U + 2q + 1) + ~V; the borrow's
       // VCC hazard costs s_nop wait states, which other waves fill: headline
       // +1.4..2.0%, NTT INV -2.2% on a paired A/B, profiles/r06/ab_bfly_sub.txt)
-      u64 nq2 = 0 - q2, q2p1 = q2 + 1, nq4 = 0 - 2 * q2;
+      const u64 q2u = uniform64(q2);
+      u64 nq2 = 0 - q2u, q2c = q2u, nq4 = 0 - 2 * q2u;
       asm("" : "+s"(nq2));
-      asm("" : "+s"(q2p1));
+      asm("" : "+s"(q2c));
       asm("" : "+s"(nq4));
       const int gs = S0 + G * LOGR + tau;  // global stage
       const bool red = !WIDE || wide_csub(gs);
@@ -425,7 +436,7 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
             A[i] = Y;
           } else {
             U[i] = harvey_csub(X + Y, nq2);
-            A[i] = (X + q2) - Y;
+            A[i] = (X + q2c) - Y;
           }
         }
         if constexpr (SP) mont_mul_sp_vec<CH>(V, A, Wt, mi.q_hi);
@@ -434,7 +445,7 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
         for (int i = 0; i < CH; ++i) {
           if (!INV) {
             x[lo_idx[c0 + i]] = U[i] + V[i];
-            x[lo_idx[c0 + i] + half] = (U[i] + q2) - V[i];
+            x[lo_idx[c0 + i] + half] = (U[i] + q2c) - V[i];
           } else {
             x[lo_idx[c0 + i]] = U[i];
             x[lo_idx[c0 + i] + half] = V[i];
@@ -445,9 +456,10 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
     }
     // generic moduli: the same lazy schedules (the generic Montgomery product
     // is below 2q and accepts any input below 8q, since 8q^2 < q 2^64)
-    u64 nq2 = 0 - q2, q2p1 = q2 + 1, nq4 = 0 - 2 * q2;
+    const u64 q2u = uniform64(q2);
+    u64 nq2 = 0 - q2u, q2c = q2u, nq4 = 0 - 2 * q2u;
     asm("" : "+s"(nq2));
-    asm("" : "+s"(q2p1));
+    asm("" : "+s"(q2c));
     asm("" : "+s"(nq4));
     const bool red = !WIDE || wide_csub(S0 + G * LOGR + tau);
 #pragma unroll
@@ -461,11 +473,11 @@ __device__ __forceinline__ void run_group(u64 (&x)[16], const u64 (&t)[16], u64 
         const u64 uu = !red ? X : harvey_csub(X, WIDE ? nq4 : nq2);
         const u64 v = mont_mul<SP>(Y, w, mi);
         X = uu + v;
-        Y = (uu + q2p1) + ~v;
+        Y = (uu + q2c) - v;
       } else {
         const u64 uu = X, vv = Y;
         X = harvey_csub(uu + vv, nq2);
-        Y = mont_mul<SP>((uu + q2p1) + ~vv, w, mi);
+        Y = mont_mul<SP>((uu + q2c) - vv, w, mi);
       }
     }
   }
@@ -567,7 +579,8 @@ __device__ __forceinline__ void group_loop(u64 (&x)[16], u64 (&tc)[16], u64 *lds
     // subtraction is one v_lshl_add_u64 with a scalar operand (left to itself
     // the compiler forms x - m as a v_subrev_co/v_subb_co borrow chain with
     // s_nop hazard padding)
-    u64 nq1 = 0 - q, nq2 = 0 - q2, nq4 = 0 - 2 * q2;
+    const u64 qu = uniform64(q);
+    u64 nq1 = 0 - qu, nq2 = 0 - 2 * qu, nq4 = 0 - 4 * qu;
     asm("" : "+s"(nq1));
     asm("" : "+s"(nq2));
     asm("" : "+s"(nq4));

@@ -363,6 +363,34 @@ def test_generic_moduli_ckks(hb):
     assert np.array_equal(hb.to_host(dout), o.rotate(a, g, k))
 
 
+@pytest.mark.parametrize("bits", [[60] * 4, [61] * 4, [60, 61, 60, 61]])
+def test_generic_moduli_c2_persistent(hb, bits):
+    """C2's shape (N=2^14, 4 limbs) on OpenFHE-style primes: the persistent
+    one-pass kernel on the generic Montgomery path (round 6) for each lazy-
+    schedule class (60-bit: wide, 61-bit: narrow), and a launch mixing both
+    (two passes), forward and inverse, against the oracle, from lazy inputs too."""
+    log_n = 14
+    mods = []
+    for b in bits:
+        mods.append(next(q for q in _generic_primes(b, log_n, len(mods) + 1) if q not in mods))
+    mods = np.array(mods, dtype=np.uint64)
+    o, c = pair(hb, SCHEME_CKKS, log_n, 4, moduli=mods)
+    x = o.uniform((9, 4, 1 << log_n), seed=sum(bits))
+    d = hb.to_device(x)
+    c.ntt_fwd(d)
+    assert np.array_equal(hb.to_host(d), o.ntt_fwd(x))
+    c.ntt_inv(d)
+    assert np.array_equal(hb.to_host(d), x)
+    d = hb.to_device(x)
+    c.ntt_inv(d)
+    assert np.array_equal(hb.to_host(d), o.ntt_inv(x))
+    q = np.asarray(o.moduli[:4], dtype=np.uint64)[None, :, None]
+    lazy = x + (np.arange(x.size, dtype=np.uint64).reshape(x.shape) % np.uint64(4)) * q  # [0, 4q)
+    d = hb.to_device(lazy)
+    c.ntt_fwd(d)
+    assert np.array_equal(hb.to_host(d), o.ntt_fwd(x))
+
+
 def test_generic_moduli_ntt_and_bfv(hb):
     log_n, L, K, dnum = 15, 3, 2, 2
     mods = np.array(_generic_primes(60, log_n, 2 * L + K + 1), dtype=np.uint64)

@@ -1,6 +1,6 @@
 """Micro-benchmark of the NTT passes and KS kernels (GPU box).
 
-    python tools/ntt_bench.py [--log-n 16] [--limbs 1152]
+    python tools/ntt_bench.py [--log-n 16] [--limbs 1152] [--openfhe-primes]
 Prints limb-NTT/s for forward and inverse transforms and the achieved
 algorithmic bandwidth (2 * N * 8 bytes per limb-NTT).
 """
@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--log-n", type=int, nargs="+", default=[14, 16])
     ap.add_argument("--limbs", type=int, default=1152)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--openfhe-primes", action="store_true", help="q = 1 mod 2N (generic Montgomery path)")
     args = ap.parse_args()
     import torch
     import herdsman_amd.backend as hb
@@ -23,7 +24,11 @@ def main():
     for log_n in args.log_n:
         n = 1 << log_n
         L = 12
-        ctx = hb.Context(hb.SCHEME_CKKS, log_n, L)
+        mods = None
+        if args.openfhe_primes:
+            from herdsman_amd.params import openfhe_style_primes
+            mods = openfhe_style_primes([(60, L)], log_n)
+        ctx = hb.Context(hb.SCHEME_CKKS, log_n, L, moduli=mods)
         s = torch.cuda.current_stream()
         ctx.set_stream(s)
         polys = max(1, args.limbs // L)
