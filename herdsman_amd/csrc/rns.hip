@@ -493,16 +493,43 @@ struct BehzDev {
 #ifndef BEHZ_COLS
 #define BEHZ_COLS 0  // 1: BEHZ dot products as 31-bit column sums (dot_cols_canon): extend +8%, floor -0.7%, C3 -0.9% (profiles/r03/ab_conv_cols.txt)
 #endif
-template <int NL, bool SP>
+// S60 (round 6): special moduli where one side of every product is below 2^60
+// (Q sources below 2^60 into Bsk targets, or Bsk sources into Q targets below
+// 2^60): 31-bit column sums reduced in place (dot_cols_sp60, < 1.25m per 4
+// terms), one reduction per 4 terms instead of a Montgomery product per term
+template <int NL>
+__device__ __forceinline__ u64 dot_sp60_canon(const u64 (&v)[NL], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
+  u64 res = 0;
+  const u64 m2 = 2 * m.q;
+#pragma unroll
+  for (int c0 = 0; c0 < NL; c0 += 4) {
+    if (c0 < (int)ns) {
+      u64 vv[4];
+      u32 h0[4], h1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool on = c0 + i < NL && c0 + i < (int)ns;
+        vv[i] = on ? v[c0 + i < NL ? c0 + i : 0] : 0;
+        if (on) split31(h[(size_t)(c0 + i) * hs], h0[i], h1[i]);
+        else h0[i] = h1[i] = 0;
+      }
+      const u64 part = dot_cols_sp60<4>(vv, h0, h1, m.q_hi);  // < 1.25m
+      res = c0 == 0 ? part : csub63(res + part, m2);            // < 2m
+    }
+  }
+  return csub63(res, m.q);
+}
+template <int NL, bool SP, bool S60 = false>
 __device__ __forceinline__ u64 behz_dot(const u64 (&v)[NL], const u64 *h, size_t hs, u32 ns, const ModInfo &m) {
-  if constexpr (BEHZ_COLS) return dot_cols_canon<NL, SP>(v, h, hs, ns, m);
+  if constexpr (SP && S60) return dot_sp60_canon<NL>(v, h, hs, ns, m);
+  else if constexpr (BEHZ_COLS) return dot_cols_canon<NL, SP>(v, h, hs, ns, m);
   else return dot_mont<NL, SP>(v, h, hs, ns, m);
 }
 
 // behz_extend (oracle): fastbconv_m_tilde then sm_mrq.  x [L] coef -> [nB] coef
 // EX: L == NL exactly (nB = L + 1 always), so every loop is unrolled with no
 // per-limb guards (the C3 parameters); otherwise NL bounds L.
-template <int NL, bool SP, bool EX>
+template <int NL, bool SP, bool EX, bool S60>
 // Poly p = 4 item + w of the BFV product's operands (w: a0, a1, b0, b1) is
 // read straight from the ciphertexts and extended to Bsk in xb [2][n][2][nB][N]
 // (the a and b parts, each in the ciphertexts' own layout).  The Q part is not
@@ -535,7 +562,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
     if (EX || j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
       // (sum_i v_i (Q/q_i) + r Q) 2^-32, the 2^-32 folded into the weights
-      const u64 xbj = behz_dot<NL, SP>(v, &bz->hx_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 xbj = behz_dot<NL, SP, S60>(v, &bz->hx_R[0][j], BEHZ_MAXL + 1, L, m);
       const u64 rr = r >= 0x80000000u ? (u64)r + m.q - (1ull << 32) : (u64)r;   // centered r mod b
       d[j * N] = csub63(xbj + csub63(mont_mul<SP>(rr, bz->qx_R[j], m), m.q), m.q);
     }
@@ -546,7 +573,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
 // The third output r2 goes straight into the key-switch scratch (the KS
 // preparation of ks_prep_kernel fused here): dc = r2 and the own-digit ext
 // slot = r2 R, so r2 is not written and read back by a separate kernel.
-template <int NL, bool SP, bool EX>
+template <int NL, bool SP, bool EX, bool S60>
 __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restrict__ eq, const u64 *__restrict__ eb,
                                                               u64 *__restrict__ out01, u64 *__restrict__ dc,
                                                               u64 *__restrict__ ext, const BehzDev *bz,
@@ -576,7 +603,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   for (int j = 0; j < NL + 1; ++j) {
     if (EX || j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
-      const u64 cv = behz_dot<NL, SP>(v, &bz->hf_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 cv = behz_dot<NL, SP, S60>(v, &bz->hf_R[0][j], BEHZ_MAXL + 1, L, m);
       const u64 tx = csub63(mont_mul<SP>(xb[j * N], bz->tf_R[j], m), m.q);
       const u64 wj = csub63(tx + cv, m.q);
       if (j == (int)nB - 1) flsk = wj;
@@ -592,7 +619,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
   u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
   for (int i = 0; i < (EX ? NL : (int)L); ++i) {
     const ModInfo m = mods[i];
-    const u64 cq = behz_dot<NL, SP>(w, &bz->h_b_q_R[0][i], BEHZ_MAXL, nB - 1, m);
+    const u64 cq = behz_dot<NL, SP, S60>(w, &bz->h_b_q_R[0][i], BEHZ_MAXL, nB - 1, m);
     const u64 ab = csub63(mont_mul<SP>(amag, bz->b_mod_q_R[i], m), m.q);
     const u64 r = csub63(cq + (neg ? ab : m.q - ab), m.q);  // cq -/+ ab (ab = 0 gives cq + q -> cq)
     // dsc (fused BFV relinearisation): dc holds ModUp's scaled sources r (Q_j/q_i)^-1
@@ -840,14 +867,22 @@ int combine_impl(fhe_ctx *c, const u64 *acc, const u64 *conv, const u64 *base, u
   return fhe_check(c, hipGetLastError(), "ks_combine_kernel");
 }
 
+// the S60 BEHZ kernels: every Q modulus below 2^60 (the other side of each of
+// their dot products is then below 2^60: dot_cols_sp60's bound)
+static bool behz_q60(const fhe_ctx *c) {
+  for (u32 i = 0; i < c->L; ++i)
+    if (c->moduli[i] >= (1ull << 60)) return false;
+  return true;
+}
+
 template <bool SP>
 int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
   dim3 grid(c->n / EW_BLOCK, 4 * n);
   const BehzDev *bz = (const BehzDev *)c->behz;
-  if (c->L == 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
-  else if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
-  else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
-  else hipLaunchKernelGGL((behz_extend_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  if (c->L == 8 && behz_q60(c)) hipLaunchKernelGGL((behz_extend_kernel<8, SP, true, true>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  else if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
+  else hipLaunchKernelGGL((behz_extend_kernel<24, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
   return fhe_check(c, hipGetLastError(), "behz_extend");
 }
 
@@ -857,10 +892,10 @@ int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *d
   dim3 grid(c->n / EW_BLOCK, n * 3);
   const BehzDev *bz = (const BehzDev *)c->behz;
   const u32 QP = c->L + c->K;
-  if (c->L == 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
-  else if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
-  else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
-  else hipLaunchKernelGGL((behz_floor_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  if (c->L == 8 && behz_q60(c)) hipLaunchKernelGGL((behz_floor_kernel<8, SP, true, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else hipLaunchKernelGGL((behz_floor_kernel<24, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
   return fhe_check(c, hipGetLastError(), "behz_floor");
 }
 

@@ -7,7 +7,7 @@ from rocprofv3 --pmc 'SQ_INSTS_VALU SQ_WAVES' runs of tools/op_bench.py
 Per kernel (name + grid): dispatches per call, waves, VALU instructions per
 wave and per ct-mult; the total per ct-mult, and each variant against the
 first.  Calls are counted by the inverse row pass with the tensor prologue
-(PRO_TENSOR / PRO_TENSOR2, one per call); the input fills and the context's
+(PRO_TENSOR / PRO_TENSOR2, one per call; BFV: the BEHZ floor / HPS scaling); the input fills and the context's
 table uploads (everything before the first fill) are excluded.
 """
 import collections
@@ -16,7 +16,9 @@ import glob
 import re
 import sys
 
-TENSOR = re.compile(r"ntt_pass<\d+, 8, 4, 16, true, false, (true|false), [25](, \d)?>")
+# one dispatch per op call: the CKKS tensor prologue (PRO_TENSOR / PRO_TENSOR2),
+# the BFV floor (BEHZ) or the HPS scaling
+TENSOR = re.compile(r"ntt_pass<\d+, 8, 4, 16, true, false, (true|false), [25](, \d)?>|behz_floor_kernel|hps_scale_kernel")
 
 
 def short(name, grid):
