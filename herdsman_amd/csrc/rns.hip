@@ -464,6 +464,88 @@ __global__ void __launch_bounds__(EW_BLOCK) automorph_ks_kernel(const u64 *__res
   ext[((size_t)(ct * ndig + j) * QP + i) * N + k] = csub63(mont_mul<SP>(y1, m.r2, m), m.q);
 }
 
+// ------------------------------------------------- base conversions on MFMA
+// BEHZ_MFMA = 1 builds the BEHZ extension and floor on the matrix cores
+// (below).  Built, bit-exact, and rejected on measurement: C3 -4.6% (floor
+// 1331 us and extension 834 us per 128-ct call against 1055 and 654 for the
+// VALU kernels).  With the sp60 column sums the VALU form costs 36 issue slots
+// per coefficient; the MFMA form spends 57 (32 coefficients per wave, half the
+// targets of each block per lane half, the combine and the per-half constant
+// selects), and neither kernel is issue-bound (profiles/r06/ab_bfv_behz_mfma.txt).
+#ifndef BEHZ_MFMA
+#define BEHZ_MFMA 0
+#endif
+#if BEHZ_MFMA
+// A fast base conversion y_t = sum_i v_i h[i][t] mod m_t over 8 sources is a
+// dense contraction, so at the BEHZ kernels' C3 shape it runs on the matrix
+// cores (v_mfma_i32_32x32x32_i8).  Sources and constants are written in 8
+// balanced signed base-256 digits (d_a = byte_a(v + 0x80..80) - 128: one 64-bit
+// add and one xor); the constant operand holds, per target t and result digit
+// b, the digits of C[i][a][t] = h[i][t] 256^a mod m_t, so that
+//   S[t][b] = sum_{i,a} d_{i,a} digit_b(C[i][a][t])     (|S| <= 64 2^14 = 2^20)
+// and y_t = mont_reduce(sum_b S[t][b] 256^b + k m_t) (constants pre-scaled by R,
+// k m_t an offset that makes the 128-bit sum non-negative).  One wave handles
+// 32 coefficients: lane (h, c) = (lane >> 5, lane & 31) supplies sources
+// {2h, 2h+1} (MFMA 0) and {4+2h, 5+2h} (MFMA 1) of coefficient c, and the
+// rows of the constant operand are ordered so that lane half h receives all 8
+// digits of targets 2h and 2h+1 of each 4-target block -- the layout of the
+// sources of the next contraction (no cross-lane exchange).  Prototype and
+// bit-check: tools/microbench/bconv_mfma.hip (round 2).
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+struct MfmaConv {
+  v4i af[3][2][64];  // [4-target block][k step (4 sources)][lane] constant operand
+  u64 off[12];       // per target: A of the offset A + 2^45 2^32 = k m_t
+};
+// this lane's source s (0..3) of an 8-source contraction
+__device__ __forceinline__ int mfma_src(int h, int s) { return (s >> 1) * 4 + 2 * h + (s & 1); }
+// the data operand of k step m from this lane's 4 source words
+__device__ __forceinline__ v4i mfma_digits(u64 x, u64 y) {
+  constexpr u64 K80 = 0x8080808080808080ull;
+  const u64 a = (x + K80) ^ K80, b = (y + K80) ^ K80;
+  return v4i{(int)(u32)a, (int)(u32)(a >> 32), (int)(u32)b, (int)(u32)(b >> 32)};
+}
+// target 2h + u of 4-target block s: its 8 result digits recombined and
+// reduced, canonical (the constants carry R: mont_reduce's R^-1 cancels it)
+__device__ __forceinline__ u64 mfma_combine(const v16i &s, int u, u64 offA, const ModInfo &m) {
+  typedef int64_t i64;
+  const int x01 = s[8 * u] + s[8 * u + 1] * 256, x23 = s[8 * u + 2] + s[8 * u + 3] * 256;
+  const int x45 = s[8 * u + 4] + s[8 * u + 5] * 256, x67 = s[8 * u + 6] + s[8 * u + 7] * 256;
+  const u64 lo = (u64)((i64)x01 + (i64)x23 * 65536) + offA;          // |.| < 2^45 before the offset
+  const u64 hi = (u64)((i64)x45 + (i64)x67 * 65536) + (1ull << 45);
+  const u64 t1 = (lo >> 32) + (u32)hi;
+  const U128 T{(u64)(u32)lo | (t1 << 32), (hi >> 32) + (t1 >> 32)};
+  return csub63(mont_reduce<true>(T, m), m.q);
+}
+// lane half h's value of a pair indexed uniformly: both loaded as scalars,
+// one select (a lane-dependent index would turn every constant and modulus
+// load of the MFMA kernels into a vector load)
+// (i0 < 0: block 2 of a 9-target contraction, target 8 only, lane half 0)
+template <class T>
+__device__ __forceinline__ T half_pick(u32 h, const T *x, int i0) {
+  if (i0 < 0) return x[8];
+  const T a = x[i0], b = x[i0 + 2];
+  return h ? b : a;
+}
+__device__ __forceinline__ ModInfo half_mod(u32 h, const ModInfo *mods, int i0) {
+  if (i0 < 0) return mods[8];
+  const ModInfo a = mods[i0], b = mods[i0 + 2];
+  ModInfo m;
+  m.q = h ? b.q : a.q;
+  m.qinv_neg = h ? b.qinv_neg : a.qinv_neg;
+  m.r2 = h ? b.r2 : a.r2;
+  m.q_hi = h ? b.q_hi : a.q_hi;
+  m.special = 1;
+  return m;
+}
+// 4-target block blk of a contraction, over both k steps
+__device__ __forceinline__ v16i mfma_conv1(const MfmaConv &f, int blk, const v4i &d0, const v4i &d1, u32 lane) {
+  const v16i z = {};
+  const v16i a = __builtin_amdgcn_mfma_i32_32x32x32_i8(f.af[blk][0][lane], d0, z, 0, 0, 0);
+  return __builtin_amdgcn_mfma_i32_32x32x32_i8(f.af[blk][1][lane], d1, a, 0, 0, 0);
+}
+#endif  // BEHZ_MFMA
+
 // ----------------------------------------------------------------- BEHZ
 // Constants for SEAL-style BEHZ (behz_init in the oracle), Montgomery
 // pre-scaled ("_R" = times 2^64 mod the modulus it is used with).
@@ -488,8 +570,34 @@ struct BehzDev {
   u64 hbm_R[BEHZ_MAXL];                // floor: (B/b_j) B^-1 mod m_sk
   u64 b_mod_q_R[BEHZ_MAXL];        // B mod q_i
   u64 h_b_q_R[BEHZ_MAXL][BEHZ_MAXL];  // (B/b_j) mod q_i
+#if BEHZ_MFMA
+  // (L = 8, special moduli): the three dense contractions on the matrix cores
+  // (behz_*_mfma_kernel): extension Q -> Bsk (hx), floor Q -> Bsk (hf), floor
+  // B -> Q (h_b_q), each 8 sources -> up to 12 targets
+  MfmaConv mx, mf, mq;
+#endif
 };
 
+// BEHZ_WPE: waves per SIMD forced on both kernels (8: -1.5% C3 against the
+// compiler's 7, profiles/r06/ab_bfv_behz_mfma.txt)
+#ifdef BEHZ_WPE
+#define BEHZ_OCC __attribute__((amdgpu_waves_per_eu(BEHZ_WPE)))
+#else
+#define BEHZ_OCC
+#endif
+#ifndef BEHZ_NT
+#define BEHZ_NT 0  // BEHZ floor: 1 = non-temporal loads, 2 = stores (1, 2, 3 all within +-0.5% of 0 on C3: ab_bfv_behz_nt.txt)
+#endif
+template <class T>
+__device__ __forceinline__ T behz_ld(const T *p) {
+  if constexpr (BEHZ_NT & 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <class T>
+__device__ __forceinline__ void behz_st(T *p, T v) {
+  if constexpr (BEHZ_NT & 2) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 #ifndef BEHZ_COLS
 #define BEHZ_COLS 0  // 1: BEHZ dot products as 31-bit column sums (dot_cols_canon): extend +8%, floor -0.7%, C3 -0.9% (profiles/r03/ab_conv_cols.txt)
 #endif
@@ -534,7 +642,7 @@ template <int NL, bool SP, bool EX, bool S60>
 // read straight from the ciphertexts and extended to Bsk in xb [2][n][2][nB][N]
 // (the a and b parts, each in the ciphertexts' own layout).  The Q part is not
 // copied: its forward NTT reads a and b out of place (bfv_mul_relin_impl).
-__global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
+__global__ void __launch_bounds__(EW_BLOCK) BEHZ_OCC behz_extend_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                                u64 *__restrict__ xb, const BehzDev *bz,
                                                                const ModInfo *mods, u32 log_n, u32 n_items) {
   const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
@@ -574,7 +682,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_extend_kernel(const u64 *__rest
 // preparation of ks_prep_kernel fused here): dc = r2 and the own-digit ext
 // slot = r2 R, so r2 is not written and read back by a separate kernel.
 template <int NL, bool SP, bool EX, bool S60>
-__global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restrict__ eq, const u64 *__restrict__ eb,
+__global__ void __launch_bounds__(EW_BLOCK) BEHZ_OCC behz_floor_kernel(const u64 *__restrict__ eq, const u64 *__restrict__ eb,
                                                               u64 *__restrict__ out01, u64 *__restrict__ dc,
                                                               u64 *__restrict__ ext, const BehzDev *bz,
                                                               const ModInfo *mods, u32 log_n, u32 QP, u32 dig_len,
@@ -591,7 +699,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
     v[i] = 0;
     if (EX || i < (int)L) {
       const ModInfo m = mods[i];
-      v[i] = csub63(mont_mul<SP>(xq[i * N], bz->t_hinv_R[i], m), m.q);  // [t x (Q/q_i)^-1]_{q_i}
+      v[i] = csub63(mont_mul<SP>(behz_ld(xq + i * N), bz->t_hinv_R[i], m), m.q);  // [t x (Q/q_i)^-1]_{q_i}
     }
   }
   // fast_floor: ((t x)_b - conv_Q->b(t x)) * Q^-1, then the fastbconv_sk
@@ -604,7 +712,7 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
     if (EX || j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
       const u64 cv = behz_dot<NL, SP, S60>(v, &bz->hf_R[0][j], BEHZ_MAXL + 1, L, m);
-      const u64 tx = csub63(mont_mul<SP>(xb[j * N], bz->tf_R[j], m), m.q);
+      const u64 tx = csub63(mont_mul<SP>(behz_ld(xb + j * N), bz->tf_R[j], m), m.q);
       const u64 wj = csub63(tx + cv, m.q);
       if (j == (int)nB - 1) flsk = wj;
       else if (j < NL) w[j] = wj;
@@ -623,10 +731,132 @@ __global__ void __launch_bounds__(EW_BLOCK) behz_floor_kernel(const u64 *__restr
     const u64 ab = csub63(mont_mul<SP>(amag, bz->b_mod_q_R[i], m), m.q);
     const u64 r = csub63(cq + (neg ? ab : m.q - ab), m.q);  // cq -/+ ab (ab = 0 gives cq + q -> cq)
     // dsc (fused BFV relinearisation): dc holds ModUp's scaled sources r (Q_j/q_i)^-1
-    o[i * N] = p == 2 && dsc ? csub63(mont_mul<SP>(r, dsc[i], m), m.q) : r;
-    if (p == 2) ext[((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k] = csub63(mont_mul<SP>(r, m.r2, m), m.q);
+    behz_st(o + i * N, p == 2 && dsc ? csub63(mont_mul<SP>(r, dsc[i], m), m.q) : r);
+    if (p == 2) behz_st(ext + ((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k, csub63(mont_mul<SP>(r, m.r2, m), m.q));
   }
 }
+
+#if BEHZ_MFMA
+// The same two kernels at L = 8 on special moduli with their dense
+// contractions on the matrix cores (MfmaConv above); bit-identical outputs
+// (every conversion is the same residue, canonical).  One wave = 32
+// coefficients, lane half h owns sources / targets {2h, 2h+1, 4+2h, 5+2h}.
+__global__ void __launch_bounds__(EW_BLOCK) behz_extend_mfma_kernel(const u64 *__restrict__ a,
+                                                                    const u64 *__restrict__ b, u64 *__restrict__ xb,
+                                                                    const BehzDev *bz, const ModInfo *mods, u32 log_n,
+                                                                    u32 n_items) {
+  constexpr int L = 8, nB = 9;
+  const u32 lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+  const u32 k = (blockIdx.x * (EW_BLOCK / 64) + (threadIdx.x >> 6)) * 32 + c;
+  const u32 p = blockIdx.y, item = p >> 2, w = p & 3;
+  const size_t N = (size_t)1 << log_n;
+  const u64 *src = (w < 2 ? a : b) + ((size_t)(2 * item + (w & 1)) * L) * N + k;
+  u64 v[4];
+  u32 xmt = 0;
+#pragma unroll
+  for (int s_ = 0; s_ < 4; ++s_) {
+    const int i = mfma_src(h, s_), i0 = mfma_src(0, s_);
+    const ModInfo m = half_mod(h, mods, i0);
+    v[s_] = csub63(mont_mul<true>(ld_nt(src + i * N), half_pick(h, bz->mt_hinv_R, i0), m), m.q);
+    xmt += (u32)v[s_] * half_pick(h, bz->h_mod_mt, i0);
+  }
+  xmt += __shfl_xor(xmt, 32);  // the other lane half's four sources
+  const u32 r = xmt * bz->neg_inv_q_mod_mt;
+  const v4i d0 = mfma_digits(v[0], v[1]), d1 = mfma_digits(v[2], v[3]);
+  u64 *d = xb + ((size_t)((w >> 1) * n_items + item) * 2 + (w & 1)) * nB * N + k;
+#pragma unroll
+  for (int blk = 0; blk < 3; ++blk) {
+    const v16i acc = mfma_conv1(bz->mx, blk, d0, d1, lane);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = 4 * blk + 2 * h + u;
+      if (j < nB) {
+        const int j0 = 4 * blk + u, jp = blk == 2 ? -1 : j0;  // block 2: j = 8 only (lane half 0)
+        const ModInfo m = half_mod(h, mods + bz->bsk0, jp);
+        const u64 xbj = mfma_combine(acc, u, half_pick(h, bz->mx.off, jp), m);
+        const u64 rr = r >= 0x80000000u ? (u64)r + m.q - (1ull << 32) : (u64)r;  // centered r mod b
+        d[j * N] = csub63(xbj + csub63(mont_mul<true>(rr, half_pick(h, bz->qx_R, jp), m), m.q), m.q);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(EW_BLOCK) behz_floor_mfma_kernel(const u64 *__restrict__ eq,
+                                                                   const u64 *__restrict__ eb, u64 *__restrict__ out01,
+                                                                   u64 *__restrict__ dc, u64 *__restrict__ ext,
+                                                                   const BehzDev *bz, const ModInfo *mods, u32 log_n,
+                                                                   u32 QP, u32 dig_len, u32 ndig, const u64 *dsc) {
+  constexpr int L = 8, nB = 9;
+  const u32 lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+  const u32 k = (blockIdx.x * (EW_BLOCK / 64) + (threadIdx.x >> 6)) * 32 + c;
+  const u32 ct = blockIdx.y / 3, p = blockIdx.y % 3;
+  const size_t N = (size_t)1 << log_n;
+  const u64 *xq = eq + ((size_t)(ct * 3 + p) * L) * N + k;
+  const u64 *xb = eb + ((size_t)(ct * 3 + p) * nB) * N + k;
+  u64 v[4];
+#pragma unroll
+  for (int s_ = 0; s_ < 4; ++s_) {
+    const int i = mfma_src(h, s_), i0 = mfma_src(0, s_);
+    const ModInfo m = half_mod(h, mods, i0);
+    v[s_] = csub63(mont_mul<true>(xq[i * N], half_pick(h, bz->t_hinv_R, i0), m), m.q);  // [t x (Q/q_i)^-1]_{q_i}
+  }
+  // fast_floor's conversion Q -> Bsk; w_j = x_b t Q^-1 c_j + conv_j (the constants carry Q^-1 c_j)
+  u64 xbv[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int j = 4 * (q >> 1) + 2 * h + (q & 1);
+    xbv[q] = j < nB ? xb[j * N] : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) asm volatile("" : "+v"(xbv[q]));
+  const v4i d0 = mfma_digits(v[0], v[1]), d1 = mfma_digits(v[2], v[3]);
+  u64 wv[6];  // w_j of this lane's targets j = 4 blk + 2 h + u (j = 8: m_sk, lane half 0)
+#pragma unroll
+  for (int blk = 0; blk < 3; ++blk) {
+    const v16i acc = mfma_conv1(bz->mf, blk, d0, d1, lane);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = 4 * blk + 2 * h + u;
+      wv[2 * blk + u] = 0;
+      if (j < nB) {
+        const int j0 = 4 * blk + u, jp = blk == 2 ? -1 : j0;  // block 2: j = 8 only (lane half 0)
+        const ModInfo m = half_mod(h, mods + bz->bsk0, jp);
+        const u64 cv = mfma_combine(acc, u, half_pick(h, bz->mf.off, jp), m);
+        const u64 tx = csub63(mont_mul<true>(xbv[2 * blk + u], half_pick(h, bz->tf_R, jp), m), m.q);
+        wv[2 * blk + u] = csub63(tx + cv, m.q);
+      }
+    }
+  }
+  // alpha = sum_{j < 8} w_j (B/b_j) B^-1 - w_msk  (mod m_sk): each lane half its 4 terms
+  const ModInfo msk = mods[bz->bsk0 + nB - 1];
+  u64 part = 0;
+#pragma unroll
+  for (int s_ = 0; s_ < 4; ++s_) part += mont_mul<true>(wv[s_], half_pick(h, bz->hbm_R, mfma_src(0, s_)), msk);  // < 6 m_sk
+  part = csub63(csub63(csub(part, 4 * msk.q), 2 * msk.q), msk.q);
+  const u64 other = __shfl_xor(part, 32);
+  const u64 flsk = __shfl(wv[4], c);  // w_8 lives in lane half 0
+  const u64 alpha = sub_mod(add_mod(part, other, msk.q), flsk, msk.q);
+  const bool neg = alpha > msk.q / 2;
+  const u64 amag = neg ? msk.q - alpha : alpha;
+  // fastbconv_sk's conversion B -> Q: this lane's w_j are exactly the sources it supplies
+  const v4i e0 = mfma_digits(wv[0], wv[1]), e1 = mfma_digits(wv[2], wv[3]);
+  u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const v16i acc = mfma_conv1(bz->mq, blk, e0, e1, lane);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = 4 * blk + 2 * h + u, i0 = 4 * blk + u;
+      const ModInfo m = half_mod(h, mods, i0);
+      const u64 cq = mfma_combine(acc, u, half_pick(h, bz->mq.off, i0), m);
+      const u64 ab = csub63(mont_mul<true>(amag, half_pick(h, bz->b_mod_q_R, i0), m), m.q);
+      const u64 rr = csub63(cq + (neg ? ab : m.q - ab), m.q);
+      o[i * N] = p == 2 && dsc ? csub63(mont_mul<true>(rr, half_pick(h, dsc, i0), m), m.q) : rr;
+      if (p == 2) ext[((size_t)(ct * ndig + i / dig_len) * QP + i) * N + k] = csub63(mont_mul<true>(rr, m.r2, m), m.q);
+    }
+  }
+}
+#endif  // BEHZ_MFMA
 
 // ------------------------------------------------------------------ HPS
 // BFV multiplication by Halevi-Polyakov-Shoup (oracle hps_*; OpenFHE BFVrns
@@ -879,6 +1109,12 @@ template <bool SP>
 int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
   dim3 grid(c->n / EW_BLOCK, 4 * n);
   const BehzDev *bz = (const BehzDev *)c->behz;
+#if BEHZ_MFMA
+  if (SP && c->L == 8 && c->n >= 128)
+    hipLaunchKernelGGL(behz_extend_mfma_kernel, dim3(c->n / 128, 4 * n), dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz,
+                       c->d_mods, c->log_n, n);
+  else
+#endif
   if (c->L == 8 && behz_q60(c)) hipLaunchKernelGGL((behz_extend_kernel<8, SP, true, true>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
   else if (c->L <= 8) hipLaunchKernelGGL((behz_extend_kernel<8, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
   else if (c->L <= 16) hipLaunchKernelGGL((behz_extend_kernel<16, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, bz, c->d_mods, c->log_n, n);
@@ -892,6 +1128,12 @@ int behz_floor_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *d
   dim3 grid(c->n / EW_BLOCK, n * 3);
   const BehzDev *bz = (const BehzDev *)c->behz;
   const u32 QP = c->L + c->K;
+#if BEHZ_MFMA
+  if (SP && c->L == 8 && c->n >= 128)
+    hipLaunchKernelGGL(behz_floor_mfma_kernel, dim3(c->n / 128, n * 3), dim3(EW_BLOCK), 0, c->stream, eq, eb, out01,
+                       dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else
+#endif
   if (c->L == 8 && behz_q60(c)) hipLaunchKernelGGL((behz_floor_kernel<8, SP, true, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
   else if (c->L <= 8) hipLaunchKernelGGL((behz_floor_kernel<8, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
   else if (c->L <= 16) hipLaunchKernelGGL((behz_floor_kernel<16, SP, false, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, bz, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
@@ -1545,6 +1787,48 @@ int rescale_impl(fhe_ctx *up, fhe_ctx *lo, const u64 *ct, u64 *out, u32 n) {
 }
 
 // ------------------------------------------------------------ BEHZ setup
+// MfmaConv constant operands for 8 sources -> targets tm (at most 12) with
+// constants cst(i, t) (Montgomery pre-scaled, < tm[t]): lane l of the operand of
+// block blk, k step m supplies row r = l & 31 -- target 4 blk + 2 ((r >> 2) & 1)
+// + (r >> 4), result digit (r & 3) + 4 ((r >> 3) & 1) -- and k = 16 (l >> 5) + jj
+// -- source 4 m + 2 (l >> 5) + (jj >> 3), digit a = jj & 7 -- (bconv_mfma.hip);
+// the offsets make recombined sums non-negative (mfma_combine)
+#if BEHZ_MFMA
+template <class F>
+static void mfma_conv_tables(MfmaConv &f, const std::vector<u64> &tm, F cst) {
+  constexpr u64 K80 = 0x8080808080808080ull;
+  typedef unsigned __int128 u128;
+  const u32 nt = (u32)tm.size();
+  for (int blk = 0; blk < 3; ++blk)
+    for (int m = 0; m < 2; ++m)
+      for (int l = 0; l < 64; ++l) {
+        const int r = l & 31, hk = l >> 5;
+        const int hr = (r >> 2) & 1, g = r >> 3, bd = (r & 3) + 4 * (g & 1), ml = 2 * hr + (g >> 1);
+        const u32 t = 4 * blk + ml;
+        uint8_t by[16];
+        for (int jj = 0; jj < 16; ++jj) {
+          const u32 i = 4 * m + 2 * hk + (jj >> 3), a = jj & 7;
+          by[jj] = 0;
+          if (t < nt) {
+            u64 s256 = 1;
+            for (u32 e = 0; e < a; ++e) s256 = host_mulmod(s256, 256, tm[t]);
+            const u64 cv = host_mulmod(cst(i, t), s256, tm[t]);  // h R 256^a mod m_t
+            by[jj] = (uint8_t)(((cv + K80) ^ K80) >> (8 * bd));
+          }
+        }
+        v4i w;
+        for (int q = 0; q < 4; ++q)
+          w[q] = (int)((u32)by[4 * q] | (u32)by[4 * q + 1] << 8 | (u32)by[4 * q + 2] << 16 | (u32)by[4 * q + 3] << 24);
+        f.af[blk][m][l] = w;
+      }
+  const u128 B32 = (u128)1 << 77;  // 2^45 2^32
+  for (u32 t = 0; t < nt; ++t) {
+    const u128 kp = ((B32 + ((u128)1 << 45)) / tm[t] + 1) * tm[t];
+    f.off[t] = (u64)(kp - B32);
+  }
+}
+#endif
+
 int behz_setup(fhe_ctx *c) {
   const u32 L = c->L, nB = c->nB, bsk0 = c->L + c->K;
   if (L > BEHZ_MAXL) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "BFV with L > 24");
@@ -1607,6 +1891,15 @@ int behz_setup(fhe_ctx *c) {
       B->hf_R[i][j] = R((b - M(h_q_bsk[i][j], qf, b)) % b, b);
     }
   }
+#if BEHZ_MFMA
+  if (L == 8 && c->special) {
+    // the MFMA contractions' constant operands (behz_*_mfma_kernel)
+    std::vector<u64> bq(qq, qq + L), bb(bsk, bsk + nB);
+    mfma_conv_tables(B->mx, bb, [&](u32 i, u32 j) { return B->hx_R[i][j]; });
+    mfma_conv_tables(B->mf, bb, [&](u32 i, u32 j) { return B->hf_R[i][j]; });
+    mfma_conv_tables(B->mq, bq, [&](u32 j, u32 i) { return B->h_b_q_R[j][i]; });
+  }
+#endif
   c->behz = ctx_upload(c, B, sizeof(BehzDev));
   delete B;
   return c->behz ? FHE_OK : FHE_ERR_OOM;

@@ -11,7 +11,7 @@
 #   abk=V1,V2,...  per-kernel A/B: rocprofv3 --kernel-trace --stats of op_bench ckks_mul per variant,
 #                  2 reps interleaved, then tools/kstat_cmp.py (op rate in each variant's log)
 #   stats          rocprofv3 --kernel-trace --stats of a short bench.py (roofline summary)
-#   steppmc        kernel trace + FETCH_SIZE + WRITE_SIZE passes of op_bench ckks_mul (128 per call):
+#   steppmc[=OP]   kernel trace + FETCH_SIZE + WRITE_SIZE passes of op_bench OP (default ckks_mul, 128 per call):
 #                  summarise here with tools/step_summary.py -> profiles/<round>/step_summary.json
 #   optrace=OP     rocprofv3 --kernel-trace --stats of tools/op_bench.py OP (bfv_mul, ckks_mul, ckks_rot)
 #   prof           tools/profile_round.sh (roofline stats, PMC passes; summarise with tools/collect_profile.py)
@@ -48,8 +48,9 @@ for s in "$@"; do
         echo "$v rep$rep $(HERD_FHE_LIB=$(lib_of $v) timeout -k 10 200 python3 tools/op_bench.py ckks_mul --batch 128 --reps 20 2>/dev/null | tail -n 1)"
       done; done > "$O/abk.txt" ;;
     stats) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/stats" -o run -- python3 bench.py --no-cpu --no-secondary --steps 3 --warmup 1 > "$O/stats.log" 2>&1 ;;
-    steppmc)
-      B="python3 tools/op_bench.py ckks_mul --batch 128"
+    steppmc|steppmc=*)
+      OPP=ckks_mul; [ "$s" = steppmc ] || OPP=${s#steppmc=}
+      B="python3 tools/op_bench.py $OPP --batch 128"
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/st_trace" -o run -- $B --reps 4 > "$O/st_trace.log" 2>&1
       timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/st_fetch" -o run -- $B --reps 2 > "$O/st_fetch.log" 2>&1
       timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/st_write" -o run -- $B --reps 2 > "$O/st_write.log" 2>&1 ;;

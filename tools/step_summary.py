@@ -4,7 +4,10 @@ a kernel trace, a FETCH_SIZE pass and a WRITE_SIZE pass (tools/gpu_steps.sh
 steppmc).  Writes profiles/step_traffic.json, which bench.py puts into its
 line as the `step` block.
 
-    python tools/step_summary.py TRACE_DIR FETCH_DIR WRITE_DIR OUT_DIR
+    python tools/step_summary.py TRACE_DIR FETCH_DIR WRITE_DIR OUT_DIR [CALL_REGEX WORKLOAD]
+
+(another op: CALL_REGEX names the kernel launched once per call, e.g.
+"behz_floor" for bfv_mul; profiles/step_traffic.json is then left alone)
 
 A call of op_bench is one wave (128 ct-mults); calls are counted by the
 PRO_TENSOR inverse row pass (one per call).  HBM bytes follow
@@ -29,7 +32,7 @@ def short(name):
     return f"{m.group(1)}<{m.group(2)}>" if m else name.split("(")[0]
 
 
-def trace(d):
+def trace(d, TENSOR=TENSOR):
     f = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
     per, calls = collections.defaultdict(lambda: [0, 0.0]), 0
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
@@ -45,7 +48,7 @@ def trace(d):
     return per, calls
 
 
-def counters(d, name, scale):
+def counters(d, name, scale, TENSOR=TENSOR):
     out, calls, seen = collections.defaultdict(float), 0, set()
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -60,10 +63,11 @@ def counters(d, name, scale):
     return out, calls
 
 
-def main(tdir, fdir, wdir, dst):
-    per, calls = trace(tdir)
-    fetch, fc = counters(fdir, "FETCH_SIZE", 1024 * 2)
-    write, wc = counters(wdir, "WRITE_SIZE", 1024)
+def main(tdir, fdir, wdir, dst, marker=None, workload=None):
+    mk = re.compile(marker) if marker else TENSOR
+    per, calls = trace(tdir, mk)
+    fetch, fc = counters(fdir, "FETCH_SIZE", 1024 * 2, mk)
+    write, wc = counters(wdir, "WRITE_SIZE", 1024, mk)
     wave = 128
     rows = []
     for k, (cnt, ms) in per.items():
@@ -76,7 +80,7 @@ def main(tdir, fdir, wdir, dst):
     tot_b = sum(r["hbm_MB_per_wave"] for r in rows) * 1e6
     res = {
         "source": os.path.relpath(dst, os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
-        "workload": "tools/op_bench.py ckks_mul --batch 128 (N=2^16, L=12, K=4, dnum=3), one stream",
+        "workload": workload or "tools/op_bench.py ckks_mul --batch 128 (N=2^16, L=12, K=4, dnum=3), one stream",
         "wave": wave, "calls_traced": calls, "calls_counted": [fc, wc],
         "kernel_ms_per_wave": round(tot_ms, 4),
         "hbm_bytes_per_wave": round(tot_b),
@@ -89,8 +93,9 @@ def main(tdir, fdir, wdir, dst):
     os.makedirs(dst, exist_ok=True)
     json.dump(res, open(os.path.join(dst, "step_summary.json"), "w"), indent=1)
     top = os.path.join(os.path.dirname(dst.rstrip("/")), "step_traffic.json")
-    json.dump({k: res[k] for k in ("source", "workload", "wave", "kernel_ms_per_wave", "hbm_bytes_per_ct_mult",
-                                   "kernel_TBps", "dominant")}, open(top, "w"), indent=1)
+    if not marker:
+      json.dump({k: res[k] for k in ("source", "workload", "wave", "kernel_ms_per_wave", "hbm_bytes_per_ct_mult",
+                                     "kernel_TBps", "dominant")}, open(top, "w"), indent=1)
     print(f"{'kernel':52s} {'grid':>9s} {'n/wave':>6s} {'ms':>7s} {'MB':>8s} {'TB/s':>6s}")
     for r in rows:
         print(f"{r['kernel']:52s} {r['grid']:9d} {r['launches_per_wave']:6.2f} {r['ms_per_wave']:7.3f} "
@@ -99,4 +104,4 @@ def main(tdir, fdir, wdir, dst):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:7])
