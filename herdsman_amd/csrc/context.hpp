@@ -255,7 +255,11 @@ int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u
 bool bfv_ks_extfree_ok(const fhe_ctx *c, u32 ndig);
 // the first (column) pass of a forward NTT alone (two-pass sizes): its
 // intermediate for a fused consumer that runs the row transforms itself
-int ntt_fwd_col_launch(fhe_ctx *c, const LimbMap &m);
+int ntt_fwd_col_launch(fhe_ctx *c, const LimbMap &m, const u64 *src = nullptr);
+// BFV mul: the forward row passes, the tensor product and the inverse row
+// passes of Q or Bsk in one kernel, then the inverse column pass (ntt_bfvt.hip)
+bool bfvt_fused_ok(const fhe_ctx *c);
+int ntt_bfv_tensor_fused_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n);
 int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, const u64 *ksk, u32 ndig,
                                const u64 *ta, const u64 *tb, u64 *out, u32 n, u32 g = 0);
 // d2_only (PRO_TENSOR2, two-pass sizes): out is not written; the ModDown

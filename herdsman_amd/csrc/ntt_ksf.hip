@@ -425,15 +425,26 @@ bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig) {
 #ifndef BFV_KS_EXTFREE
 #define BFV_KS_EXTFREE 1  // BFV: ModUp's row transforms inside the all-limb inner-product pass (ksp_fused_pass)
 #endif
-int ntt_fwd_col_launch(fhe_ctx *c, const LimbMap &m) {
+int ntt_fwd_col_launch(fhe_ctx *c, const LimbMap &m, const u64 *src) {
   if (c->log_n < 15) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "column pass alone: log_n");
-  NttArgs a{};
-  a.map = m;
-  a.tw = c->d_tw_fwd;
-  a.mods = c->d_mods;
-  a.ninv = c->d_ninv;
-  a.log_n = c->log_n;
-  return m.n_polys * m.cnt ? ntt_col_plain(c, a, false, m.n_polys * m.cnt) : FHE_OK;
+  const u32 per = 65535u;  // polys per launch (gridDim.y)
+  for (u32 p0 = 0; p0 < m.n_polys; p0 += per) {
+    const size_t off = (size_t)p0 * m.poly_stride * c->n;
+    NttArgs a{};
+    a.map = m;
+    a.map.base = m.base + off;
+    a.map.n_polys = std::min(per, m.n_polys - p0);
+    a.src = src ? src + off : nullptr;  // out of place: the column pass reads src, writes map
+    a.tw = c->d_tw_fwd;
+    a.mods = c->d_mods;
+    a.ninv = c->d_ninv;
+    a.log_n = c->log_n;
+    if (a.map.cnt) {
+      const int rc = ntt_col_plain(c, a, false, a.map.n_polys * a.map.cnt);
+      if (rc) return rc;
+    }
+  }
+  return FHE_OK;
 }
 
 bool bfv_ks_extfree_ok(const fhe_ctx *c, u32 ndig) {

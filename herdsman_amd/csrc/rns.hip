@@ -1972,6 +1972,16 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   //      HPS (the exact centred lift, fhe_params.flags FHE_FLAG_BFV_HPS)
   if ((rc = c->hps ? SP_DISPATCH(c, hps_extend_impl, c, a, b, xb, n) : SP_DISPATCH(c, behz_extend_impl, c, a, b, xb, n)))
     return rc;
+  // 3-4 fused (BFVT): the forward column passes here (the Q part out of place,
+  //    straight from the ciphertexts); the forward row passes, the tensor and
+  //    the inverse row passes in one kernel per base, then the inverse column passes
+  if (bfvt_fused_ok(c)) {
+    if ((rc = ntt_fwd_col_launch(c, LimbMap{xq, L, L, 0, L, 0, 0, 2 * n}, a))) return rc;
+    if ((rc = ntt_fwd_col_launch(c, LimbMap{xq + (size_t)n * 2 * L * N, L, L, 0, L, 0, 0, 2 * n}, b))) return rc;
+    if ((rc = ntt_fwd_col_launch(c, LimbMap{xb, nB, nB, 0, nB, 0, bsk0, 4 * n}))) return rc;
+    if ((rc = ntt_bfv_tensor_fused_launch(c, xq, xq + (size_t)n * 2 * L * N, eq, L, 0, n))) return rc;
+    if ((rc = ntt_bfv_tensor_fused_launch(c, xb, xb + (size_t)n * 2 * nB * N, eb, nB, bsk0, n))) return rc;
+  } else {
   // 3. NTT in Q and Bsk
   //    (the Q part out of place, straight from the ciphertexts)
   if ((rc = ntt_launch(c, LimbMap{xq, L, L, 0, L, 0, 0, 2 * n}, false, false, false, nullptr, a))) return rc;
@@ -1983,6 +1993,7 @@ int bfv_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, u
   //    (unscaled: behz_floor's t constants carry N^-1)
   if ((rc = ntt_inv_bfv_tensor_launch(c, xq, xq + (size_t)n * 2 * L * N, eq, L, 0, n))) return rc;
   if ((rc = ntt_inv_bfv_tensor_launch(c, xb, xb + (size_t)n * 2 * nB * N, eb, nB, bsk0, n))) return rc;
+  }
   // 5. scale and round: r0, r1 -> out; r2 -> the key-switch scratch, prepared
   //    (BEHZ floor, or HPS simple scaling + exact P -> Q)
   const u64 *dsc = bfv_fused(c) ? c->d_bfv_dscale : nullptr;
