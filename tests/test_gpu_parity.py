@@ -642,6 +642,26 @@ def test_bfv_mul_relin_fused_tensor_sizes(hb, log_n, L, K, dnum):
     assert np.array_equal(hb.to_host(da), want)
 
 
+@pytest.mark.parametrize("bits", [0, 60, 61])
+def test_bfv_fused_tensor_row_passes_edge_values(hb, bits):
+    """BFV mul+relin at N=2^15 runs the forward row passes, the tensor product
+    and the inverse row passes in one kernel per base (bfvt_fused_pass,
+    ntt_bfvt.hip): edge residues (0, 1, q-1, 2^32 multiples, a zero ciphertext)
+    on the default special primes (bits 0) and on generic primes of both
+    lazy-schedule classes (60: wide, 61: narrow), plus an in-place call."""
+    log_n, L, K, dnum = 15, 3, 2, 2
+    mods = np.array(_generic_primes(bits, log_n, 2 * L + K + 1), dtype=np.uint64) if bits else None
+    o, c = pair(hb, SCHEME_BFV, log_n, L, K, dnum, t=65537, moduli=mods)
+    a = _edge_inputs(o, (2, 2, L, 1 << log_n), seed=170 + bits)
+    b = _edge_inputs(o, (2, 2, L, 1 << log_n), seed=171 + bits)
+    b[1] = 0
+    rlk = o.uniform(o.key_shape(), seed=172 + bits)
+    want = o.mul_relin(a, b, rlk)
+    da = hb.to_device(a)
+    c.mul_relin(da, hb.to_device(b), hb.to_device(rlk), da)
+    assert np.array_equal(hb.to_host(da), want)
+
+
 def test_generic_moduli_metric_size(hb):
     """OpenFHE-style primes at the metric parameters (N=2^16, L=12, K=4, dnum=3;
     60-bit Q on the wide lazy schedule, 61-bit P on the narrow one): the fused
