@@ -39,7 +39,14 @@
 #define KSP_LSW 2  // the same for the P side (6-9 VGPRs spill, outside the loops: addresses for the INTT phase)
 #endif
 #ifndef KSF_MINW
-#define KSF_MINW 3  // minimum waves per SIMD (the accumulators take 64 VGPRs)
+// minimum waves per SIMD (the accumulators take 64 VGPRs).  2, not 3: the
+// metric instantiation still allocates 168 VGPRs (3 waves) but without the
+// 5 spills the 3-wave bound produced: ksf_pass 1.90 -> 1.83 ms per wave,
+// ct-mult +0.8%, headline +0.4% (profiles/r06/ab_ksf_minw.txt)
+#define KSF_MINW 2
+#endif
+#ifndef KSP_MINW
+#define KSP_MINW 3  // the P side (2: 187 VGPRs, 2 waves, 0.61 -> 0.68 ms)
 #endif
 
 namespace {
@@ -276,7 +283,7 @@ int ksf_dispatch(fhe_ctx *c, const KsfArgs &a, u32 n) {
 // the own digit's slot holds the column-pass intermediate of the limb's own
 // d R -- so BFV's ext is never written by a row pass and never read back.
 template <int LOG_N, int KD, bool WIDE, bool SP>
-__global__ void __launch_bounds__(256, KSF_MINW) ksp_fused_pass(KspArgs a) {
+__global__ void __launch_bounds__(256, KSP_MINW) ksp_fused_pass(KspArgs a) {
   constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
   using G0 = Grp<S, LOGR, 0>;
   using G1 = Grp<S, LOGR, 1>;
