@@ -48,6 +48,9 @@
 #ifndef KSP_MINW
 #define KSP_MINW 3  // the P side (2: 187 VGPRs, 2 waves, 0.61 -> 0.68 ms)
 #endif
+#ifndef KSP_MINW15
+#define KSP_MINW15 KSP_MINW  // the same at N = 2^15 (BFV C3's all-limb pass)
+#endif
 
 namespace {
 
@@ -283,7 +286,7 @@ int ksf_dispatch(fhe_ctx *c, const KsfArgs &a, u32 n) {
 // the own digit's slot holds the column-pass intermediate of the limb's own
 // d R -- so BFV's ext is never written by a row pass and never read back.
 template <int LOG_N, int KD, bool WIDE, bool SP>
-__global__ void __launch_bounds__(256, KSP_MINW) ksp_fused_pass(KspArgs a) {
+__global__ void __launch_bounds__(256, LOG_N == 15 ? KSP_MINW15 : KSP_MINW) ksp_fused_pass(KspArgs a) {
   constexpr int S = 8, LOGR = 4, W = 16, R = 16, S0 = LOG_N - S;
   using G0 = Grp<S, LOGR, 0>;
   using G1 = Grp<S, LOGR, 1>;
