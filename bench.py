@@ -329,7 +329,7 @@ def main():
 
     secondary = None
     if full_secondary:
-        secondary = secondary_configs(hb, ctx, rlk, a, b, out, dev, stream, B, max(2, args.steps // 2))
+        secondary = secondary_configs(hb, ctx, rlk, a, b, out, dev, stream, B, max(2, 2 * args.steps))
 
     cpu = None
     if rank == 0 and world == 1 and not (args.no_cpu or args.roofline_only):
