@@ -209,6 +209,7 @@ struct TensorSrc {
   const u64 *a, *b;
   bool fused;  // the whole finish in one kernel (ntt_ks_fused_finish_launch); ModUp skips its Q row passes
   u32 g = 0;   // fused only: a CKKS rotation by g instead (a = the ciphertexts, read through sigma_g; b unused)
+  bool convf = false;  // fused only: ModUp and ModDown as CONVF launches (dc holds INTT(d2)'s row-pass output)
 };
 // Hoisted rotations of few ciphertexts: nr Galois elements' gather passes in
 // one launch (poly p of the batch = rotation p / (2 n), ciphertext poly p % (2 n))
@@ -231,7 +232,7 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
 // ksf_scale (q_rows false only): the Q targets at the fused CKKS finish's
 // scale (modup_tabs_ksf); else every target times R (modup_tabs; BFV)
 int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows = true,
-                         bool ksf_scale = true);
+                         bool ksf_scale = true, const u64 *src_rows_scale = nullptr);
 int ntt_inv_bfv_tensor_launch(fhe_ctx *c, const u64 *xa, const u64 *xb, u64 *e, u32 nl, u32 mod_offset, u32 n);
 // INTT(acc_P) with the P limbs' key-switching inner product in its first pass
 // (ext_g != 0: ext is read as sigma_g(ext), the hoisted rotation's inner product)
@@ -250,7 +251,22 @@ bool ks_fused_finish_ok(const fhe_ctx *c, u32 ndig);
 // (all_limbs: BFV -- every Q u P limb, each digit's column-pass intermediates
 // own limbs included, INTT output constants d_bfv_kscale)
 int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig,
-                         bool all_limbs = false);
+                         bool all_limbs = false, bool skip_col = false);
+// CONVF (ntt_convf.hip): an inverse NTT's column pass (sources: its row pass's
+// output, scaled on the way out), a base conversion and the forward column
+// pass of every target, in one kernel per (column block, poly)
+struct ConvfArgs {
+  const u64 *src;                        // [n_polys][src_stride][N] the inverse's row-pass output
+  u32 src_stride, src_first, src_mod0;   // source limb i: src_first + i, modulus src_mod0 + i
+  const u64 *scale;                      // per modulus: the inverse's output scale
+  LimbMap tmap;                          // the targets (their forward column-pass outputs)
+  const u64 *h;                          // the conversion table (ConvTab::h, nd targets)
+  u32 nd, src60;
+  const ModInfo *mods;
+  const u64 *twi, *twf;
+};
+bool convf_ok(const fhe_ctx *c, u32 ns);
+int ntt_convf_launch(fhe_ctx *c, const ConvfArgs &a, u32 ns);
 // the BFV key switch without a stored ext applies (ntt_ksf.hip)
 bool bfv_ks_extfree_ok(const fhe_ctx *c, u32 ndig);
 // the first (column) pass of a forward NTT alone (two-pass sizes): its
@@ -265,7 +281,7 @@ int ntt_ks_fused_finish_launch(fhe_ctx *c, const u64 *conv, const u64 *ext, cons
 // d2_only (PRO_TENSOR2, two-pass sizes): out is not written; the ModDown
 // finish forms d0 and d1 (ntt_fwd_combine_launch with a TensorSrc)
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig,
-                          bool d2_only = false);
+                          bool d2_only = false, bool rows_only = false);
 // RNS kernels (rns.hip)
 enum class EwOp { Add, Sub, Mul };
 int ew_launch(fhe_ctx *c, EwOp op, const u64 *a, const u64 *b, u64 *out, u32 n_polys, u32 mod_begin, u32 n_limbs);

@@ -9,7 +9,7 @@
 // d2_only: out and ext are left alone (PRO_TENSOR2: only a1 and b1 are read;
 // EPI_KSQT forms d0, d1 and the own digit's ext word d2 R).
 int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 *dc, u64 *ext, u32 n, u32 ndig,
-                          bool d2_only) {
+                          bool d2_only, bool rows_only) {
   const u32 L = c->L, QP = c->L + c->K;
   const size_t N = c->n;
   if (d2_only && c->log_n <= 14) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "split tensor product: log_n");
@@ -45,7 +45,8 @@ int ntt_inv_tensor_launch(fhe_ctx *c, const u64 *a, const u64 *b, u64 *out, u64 
     } else {
       if ((rc = d2_only ? row_pass<PRO_TENSOR2>(c, t, true, n_jobs) : row_pass<PRO_TENSOR>(c, t, true, n_jobs)))
         return rc;
-      rc = ntt_col_plain(c, t, true, n_jobs);
+      // rows_only: the column pass runs inside ModUp's CONVF launches (ntt_convf.hip)
+      rc = rows_only ? FHE_OK : ntt_col_plain(c, t, true, n_jobs);
     }
     if (rc) return rc;
   }

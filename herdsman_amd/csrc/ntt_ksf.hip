@@ -464,7 +464,9 @@ bool bfv_ks_extfree_ok(const fhe_ctx *c, u32 ndig) {
 // INTT(acc_P) with the P limbs' ModUp row transforms and inner product fused
 // into its first pass (ksp_fused_pass), then its column pass (d_iscale), as
 // ntt_inv_ksp_launch leaves acc's P rows
-int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, bool all_limbs) {
+// skip_col (CONVF): the column pass runs inside ModDown's CONVF launch instead
+int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u32 n, u32 ndig, bool all_limbs,
+                         bool skip_col) {
   if (!ks_fused_finish_ok(c, ndig)) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused P-limb key switch: shape");
   if (all_limbs && !bfv_ks_extfree_ok(c, ndig))
     return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused all-limb key switch: BFV tables");
@@ -499,6 +501,7 @@ int ntt_ksp_fused_launch(fhe_ctx *c, u64 *acc, const u64 *ext, const u64 *ksk, u
       }
     }
     if (rc) return rc;
+    if (skip_col && !all_limbs) continue;
     NttArgs a{};
     a.map = all_limbs ? LimbMap{k.acc, QP, QP, 0, QP, 0, 0, 2 * nc} : LimbMap{k.acc, QP, K, L, QP, 0, 0, 2 * nc};
     a.tw = c->d_tw_inv;

@@ -9,7 +9,11 @@
 // INTT through d_iscale) as its prologue (PRO_CONV), so the converted limbs
 // never make an HBM round trip; the row pass leaves lazy outputs (< 8q) for
 // the inner product on special moduli, as keyswitch_run's separate NTT does.
-int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows, bool ksf_scale) {
+// src_rows_scale (CONVF, the fused key switch): dc holds INTT(d2)'s ROW-pass
+// output; its column pass (output scale src_rows_scale) runs in the same
+// kernel as the conversion and the targets' column passes (ntt_convf.hip).
+int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u32 j, bool q_rows, bool ksf_scale,
+                         const u64 *src_rows_scale) {
   const u32 L = c->L, QP = c->L + c->K, N = c->n;
   const u32 lo = j * c->alpha, hi = std::min(lo + c->alpha, L);
   // q_rows false (the fused key switch): Q targets at its accumulator scale
@@ -17,6 +21,8 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
   if (ksf && c->modup_tabs_ksf.size() <= j) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp: ksf tables");
   const ConvTab &tab = ksf ? c->modup_tabs_ksf[j] : c->modup_tabs[j];
   if (c->log_n <= 14 || tab.ns > 4) return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp: log_n / digit size");
+  if (src_rows_scale && (q_rows || !convf_ok(c, tab.ns)))
+    return fhe_fail(c, FHE_ERR_UNSUPPORTED, "fused ModUp from row-pass sources: shape");
   const u32 per = 65535u;  // gridDim.y
   for (u32 p0 = 0; p0 < n; p0 += per) {
     const u32 np = std::min(per, n - p0);
@@ -46,7 +52,22 @@ int ntt_fwd_modup_launch(fhe_ctx *c, const u64 *dc, u64 *ext, u32 n, u32 ndig, u
     ap.c_h = tab.h + (L - (hi - lo));
     const int wq = wide_mode(c, aq.map), wp = wide_mode(c, ap.map);
     int rc;
-    if (!q_rows) {
+    if (!q_rows && src_rows_scale) {
+      ConvfArgs f{};
+      f.src = a.c_src;
+      f.src_stride = L;
+      f.src_first = lo;
+      f.src_mod0 = lo;
+      f.scale = src_rows_scale;
+      f.tmap = a.map;
+      f.h = tab.h;
+      f.nd = tab.nd;
+      f.src60 = a.c_src60;
+      f.mods = c->d_mods;
+      f.twi = c->d_tw_inv;
+      f.twf = c->d_tw_fwd;
+      rc = ntt_convf_launch(c, f, tab.ns);
+    } else if (!q_rows) {
       // the fused key switch transforms every target's rows itself (ntt_ksf.hip)
       rc = ntt_conv_col(c, a, n_jobs);
     } else if (wq != 2 && wp != 2 && wq != wp && aq.map.cnt && ap.map.cnt) {

@@ -88,7 +88,26 @@ int ntt_fwd_combine_launch(fhe_ctx *c, u64 *conv, u32 n_polys, const u64 *acc, u
         a.c_ns = pro->ns;
         a.c_nd = pro->nd;
         a.c_h = pro->h;
-        rc = ntt_conv_col(c, a, n_jobs);
+        if (tsrc && tsrc->convf && !pro_src) {
+          // CONVF: acc's P rows hold INTT(acc_P)'s row-pass output; its column
+          // pass (d_iscale) runs in the conversion's kernel (ntt_convf.hip)
+          ConvfArgs f{};
+          f.src = a.c_src;
+          f.src_stride = acc_stride;
+          f.src_first = L;
+          f.src_mod0 = L;
+          f.scale = c->d_iscale;
+          f.tmap = a.map;
+          f.h = pro->h;
+          f.nd = pro->nd;
+          f.src60 = 0;
+          f.mods = c->d_mods;
+          f.twi = c->d_tw_inv;
+          f.twf = c->d_tw_fwd;
+          rc = ntt_convf_launch(c, f, pro->ns);
+        } else {
+          rc = ntt_conv_col(c, a, n_jobs);
+        }
       } else {
         rc = ntt_col_plain(c, a, false, n_jobs);
       }

@@ -1259,7 +1259,10 @@ static KsWs ks_layout(const fhe_ctx *c, u32 n, u64 *ws) {
 // Split in two for hoisted rotations: ks_extend (steps 1-3: INTT, ModUp, NTT of
 // the converted limbs, into w.ext) runs once per input, ks_finish (steps 4-6:
 // inner product, ModDown) once per key.
-static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is_coef, bool q_rows = true) {
+// rows_scale (CONVF): dc holds INTT(d)'s row-pass output, whose column pass
+// (output scale rows_scale) runs inside ModUp's CONVF launches
+static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is_coef, bool q_rows = true,
+                     const u64 *rows_scale = nullptr) {
   const u32 L = c->L, QP = L + c->K, N = c->n, ndig = w.ndig;
   u64 *dc = w.dc, *ext = w.ext;
   int rc;
@@ -1274,7 +1277,7 @@ static int ks_extend(fhe_ctx *c, const KsWs &w, u32 n, bool ntt_form, bool dc_is
   if (fused_modup) {
     // 2-3. ModUp + NTT of the converted limbs, one digit at a time
     for (u32 j = 0; j < ndig; ++j)
-      if ((rc = ntt_fwd_modup_launch(c, dc, ext, n, ndig, j, q_rows))) return rc;
+      if ((rc = ntt_fwd_modup_launch(c, dc, ext, n, ndig, j, q_rows, true, rows_scale))) return rc;
   }
   if (!q_rows && !fused_modup) return fhe_fail(c, FHE_ERR_INVALID, "ModUp without Q rows: fused ModUp only");
   // 2. ModUp: every non-own limb of every digit
@@ -1317,7 +1320,7 @@ static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, 
   //      conversion in its first pass and the combine in its last
   //      (out = base + (acc_Q - conv) P^-1): conv never makes an HBM round trip
   if (ntt_form && c->fuse_moddown) {
-    if (tsrc && tsrc->fused) rc = ntt_ksp_fused_launch(c, acc, ext, ksk, n, ndig);
+    if (tsrc && tsrc->fused) rc = ntt_ksp_fused_launch(c, acc, ext, ksk, n, ndig, false, tsrc->convf);
     else if (ksq && KSP_FUSE) rc = ntt_inv_ksp_launch(c, acc, ext, ksk, n, ndig, ext_g);
     else rc = ntt_launch(c, LimbMap{acc, QP, K, L, QP, 0, 0, 2 * n}, true, false, false, c->d_iscale);
     if (rc) return rc;
@@ -1339,7 +1342,8 @@ static int ks_finish(fhe_ctx *c, const KsWs &w, const u64 *ext, const u64 *ksk, 
 
 static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *base, u64 *out, u32 n, u32 add_mask,
                          bool ntt_form, bool dc_is_coef = false, u32 base_g = 0, const TensorSrc *tsrc = nullptr) {
-  int rc = ks_extend(c, w, n, ntt_form, dc_is_coef, !(tsrc && tsrc->fused));
+  const u64 *rows_scale = tsrc && tsrc->convf ? c->d_iscale_t : nullptr;  // INTT(d2)'s scale (ntt_inv_tensor_launch)
+  int rc = ks_extend(c, w, n, ntt_form, dc_is_coef, !(tsrc && tsrc->fused), rows_scale);
   return rc ? rc : ks_finish(c, w, w.ext, ksk, base, out, n, add_mask, ntt_form, base_g, 0, tsrc);
 }
 
@@ -1451,8 +1455,11 @@ int ckks_mul_relin_impl(fhe_ctx *c, const u64 *a, const u64 *b, const u64 *rlk, 
   const bool pre = TENSOR_SPLIT && c->log_n > 14 && c->fuse_moddown && w.ndig <= 3 && KSP_FUSE && apart;
   const bool fused = pre && c->fuse_modup && ks_fused_finish_ok(c, w.ndig);
   const bool split = fused || (pre && c->special);
-  if ((rc = ntt_inv_tensor_launch(c, a, b, out, w.dc, w.ext, n, w.ndig, split))) return rc;
-  const TensorSrc ts{a, b, fused};
+  // CONVF: INTT(d2)'s and INTT(acc_P)'s column passes run inside the ModUp and
+  // ModDown conversion kernels (ntt_convf.hip): 4-limb digits and 4 P limbs
+  const bool cf = fused && c->d_iscale_t && c->L % c->alpha == 0 && convf_ok(c, c->alpha) && convf_ok(c, c->K);
+  if ((rc = ntt_inv_tensor_launch(c, a, b, out, w.dc, w.ext, n, w.ndig, split, cf))) return rc;
+  const TensorSrc ts{a, b, fused, 0, cf};
   return keyswitch_run(c, w, rlk, out, out, n, 3u, true, true, 0, split ? &ts : nullptr);
 }
 
