@@ -585,6 +585,23 @@ struct BehzDev {
 #else
 #define BEHZ_OCC
 #endif
+#ifndef BEHZ_FENCES
+#define BEHZ_FENCES 1
+#endif
+// a scheduling fence per target of the BEHZ kernels: left free, the scheduler
+// hoists every target's uniform constants (hx / hf, h_b_q: up to 136 words,
+// split into 31-bit digits) to the top, past the 102 SGPRs, and spills them to
+// VGPR lanes (v_writelane / v_readlane).  Fenced, the extension drops 13% of its
+// VALU instructions and runs at 36 VGPRs (8 waves): 650 -> 555 us per C3 call.
+// The floor's fences (bits 2, 4) remove its 104 SGPR spills too but cost 2% of
+// C3 (its Bsk loads can no longer run ahead of the previous target's products,
+// also with a one-ahead prefetch): profiles/r06/ab_behz_fences.txt
+// BEHZ_FENCES bits: 1 the extension's targets, 2 the floor's Bsk targets, 4 the floor's Q targets,
+// 8 the HPS extension's targets
+#define BEHZ_FENCE(bit)                                          \
+  do {                                                           \
+    if constexpr (BEHZ_FENCES & (bit)) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
 #ifndef BEHZ_NT
 #define BEHZ_NT 0  // BEHZ floor: 1 = non-temporal loads, 2 = stores (1, 2, 3 all within +-0.5% of 0 on C3: ab_bfv_behz_nt.txt)
 #endif
@@ -667,6 +684,7 @@ __global__ void __launch_bounds__(EW_BLOCK) BEHZ_OCC behz_extend_kernel(const u6
   constexpr int UJ = EX ? NL + 1 : 1;  // unrolled only with compile-time bounds
 #pragma unroll UJ
   for (int j = 0; j < NL + 1; ++j) {
+    BEHZ_FENCE(1);
     if (EX || j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
       // (sum_i v_i (Q/q_i) + r Q) 2^-32, the 2^-32 folded into the weights
@@ -709,6 +727,7 @@ __global__ void __launch_bounds__(EW_BLOCK) BEHZ_OCC behz_floor_kernel(const u64
   u64 flsk = 0;
 #pragma unroll
   for (int j = 0; j < NL + 1; ++j) {
+    BEHZ_FENCE(2);
     if (EX || j < (int)nB) {
       const ModInfo m = mods[bz->bsk0 + j];
       const u64 cv = behz_dot<NL, SP, S60>(v, &bz->hf_R[0][j], BEHZ_MAXL + 1, L, m);
@@ -726,6 +745,7 @@ __global__ void __launch_bounds__(EW_BLOCK) BEHZ_OCC behz_floor_kernel(const u64
   const u64 amag = neg ? msk.q - alpha : alpha;
   u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
   for (int i = 0; i < (EX ? NL : (int)L); ++i) {
+    BEHZ_FENCE(4);
     const ModInfo m = mods[i];
     const u64 cq = behz_dot<NL, SP, S60>(w, &bz->h_b_q_R[0][i], BEHZ_MAXL, nB - 1, m);
     const u64 ab = csub63(mont_mul<SP>(amag, bz->b_mod_q_R[i], m), m.q);
@@ -925,6 +945,7 @@ __global__ void __launch_bounds__(EW_BLOCK) hps_extend_kernel(const u64 *__restr
   constexpr int UJ = EX ? NL + 1 : 1;
 #pragma unroll UJ
   for (int j = 0; j < NL + 1; ++j) {
+    BEHZ_FENCE(8);
     if (EX || j < (int)nB) {
       const ModInfo m = mods[hp->bsk0 + j];
       const u64 x = dot_mont<NL, SP>(y, &hp->qstar_R[0][j], BEHZ_MAXL + 1, L, m);

@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("op", choices=["bfv_mul", "ckks_mul", "ckks_rot", "ckks_hrot", "bfv_rot", "bfv_hrot",
+    ap.add_argument("op", choices=["bfv_mul", "bfv_hps_mul", "ckks_mul", "ckks_rot", "ckks_hrot", "bfv_rot", "bfv_hrot",
                                        "ckks_rsum", "bfv_rsum", "ckks_lin"])
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=10)
@@ -31,7 +31,11 @@ def main():
     import herdsman_amd.backend as hb
 
     if args.op.startswith("bfv"):
-        c = hb.Context(hb.SCHEME_BFV, 15, 8, 4, 2, t=65537)
+        # bfv_hps_*: the HPS multiplication (fhe_params FHE_FLAG_BFV_HPS)
+        kw = {"bfv_mult": "hps"} if args.op.startswith("bfv_hps") else {}
+        c = hb.Context(hb.SCHEME_BFV, 15, 8, 4, 2, t=65537, **kw)
+        if args.op.startswith("bfv_hps"):
+            args.op = "bfv" + args.op[len("bfv_hps"):]
     else:
         mods = None
         if args.openfhe_primes:
