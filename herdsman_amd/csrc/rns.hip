@@ -471,7 +471,9 @@ __global__ void __launch_bounds__(EW_BLOCK) automorph_ks_kernel(const u64 *__res
 // VALU kernels).  With the sp60 column sums the VALU form costs 36 issue slots
 // per coefficient; the MFMA form spends 57 (32 coefficients per wave, half the
 // targets of each block per lane half, the combine and the per-half constant
-// selects), and neither kernel is issue-bound (profiles/r06/ab_bfv_behz_mfma.txt).
+// selects), and both kernels are VALU-issue bound (busy 1.04 / 0.98,
+// profiles/r06/stall_c3.txt), so the extra slots cost time directly
+// (profiles/r06/ab_bfv_behz_mfma.txt).
 #ifndef BEHZ_MFMA
 #define BEHZ_MFMA 0
 #endif
