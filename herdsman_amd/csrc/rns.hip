@@ -1370,6 +1370,61 @@ static int keyswitch_run(fhe_ctx *c, const KsWs &w, const u64 *ksk, const u64 *b
   return rc ? rc : ks_finish(c, w, w.ext, ksk, base, out, n, add_mask, ntt_form, base_g, 0, tsrc);
 }
 
+// BFV_MD_COEF: one thread per coefficient of a poly forms all L outputs (the
+// K P-limb sources read once into registers instead of once per output limb
+// through L2)
+#ifndef BFV_MD_COEF
+#define BFV_MD_COEF 1
+#endif
+namespace {
+template <bool SP>
+__global__ void __launch_bounds__(EW_BLOCK) bfv_moddown_coef_kernel(const u64 *__restrict__ acc, const u64 *base,
+                                                                    u64 *out, const u64 *__restrict__ h,
+                                                                    const u64 *pinv, const ModInfo *mods, u32 L,
+                                                                    u32 K, u32 QP, u32 log_n, u32 add_mask,
+                                                                    u32 base_ginv, BfvRotOut ro) {
+  const u32 k = blockIdx.x * EW_BLOCK + threadIdx.x;
+  const u32 p = blockIdx.y;  // 2 ct + b (of the rotation batch)
+  u32 cp = p;
+  if (ro.rp) {
+    const u32 r = p / ro.rp;
+    cp = p - r * ro.rp;
+    out = ro.out[r];
+    base_ginv = ro.ginv[r];
+  }
+  const size_t N = (size_t)1 << log_n;
+  const u64 *ap = acc + (size_t)p * QP * N + k;
+  u64 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = j < (int)K ? ap[(size_t)(L + j) * N] : 0;
+  const bool add = add_mask & (1u << (p & 1));
+  const u32 n = 1u << log_n, j0 = (u32)(((u64)k * base_ginv) & (2 * n - 1));
+  for (u32 i = 0; i < L; ++i) {
+    const ModInfo m = mods[i];
+    u32 h0[4], h1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < (int)K) split31(h[(size_t)j * L + i], h0[j], h1[j]);
+      else h0[j] = h1[j] = 0;
+    }
+    const u64 cv = csub63(dot_cols<4, SP>(v, h0, h1, m), m.q);
+    u64 ks = csub63(mont_mul<SP>(sub_mod(ap[(size_t)i * N], cv, m.q), pinv[i], m), m.q);
+    const size_t o = ((size_t)cp * L + i) * N + k;
+    if (add) {
+      u64 bv;
+      if (base_ginv) {
+        const u64 *bp = base + ((size_t)cp * L + i) * N;
+        bv = j0 < n ? bp[j0] : (bp[j0 - n] ? m.q - bp[j0 - n] : 0);
+      } else {
+        bv = base[o];
+      }
+      ks = add_mod(ks, bv, m.q);
+    }
+    out[o] = ks;
+  }
+}
+}  // namespace
+
 template <bool SP>
 static int bfv_moddown_impl(fhe_ctx *c, const u64 *acc, const u64 *base, u64 *out, u32 n, u32 add_mask,
                             u32 base_ginv, const RotBatch *rb = nullptr) {
@@ -1385,6 +1440,12 @@ static int bfv_moddown_impl(fhe_ctx *c, const u64 *acc, const u64 *base, u64 *ou
       ro.out[r] = rb->out[r];
       ro.ginv[r] = galois_inv(rb->g[r], c->log_n);
     }
+  }
+  if (BFV_MD_COEF && c->K <= 4 && 2 * n * nr <= kMaxGridY) {
+    hipLaunchKernelGGL((bfv_moddown_coef_kernel<SP>), dim3(c->n / EW_BLOCK, 2 * n * nr), dim3(EW_BLOCK), 0,
+                       c->stream, acc, base, rb ? nullptr : out, c->moddown.h, c->d_pinv, c->d_mods, L, c->K,
+                       (u32)QP, c->log_n, add_mask, base_ginv, ro);
+    return fhe_check(c, hipGetLastError(), "bfv_moddown_coef_kernel");
   }
   for (u32 p0 = 0; p0 < 2 * n * nr; p0 += per) {
     const u32 np = std::min(per, 2 * n * nr - p0);
