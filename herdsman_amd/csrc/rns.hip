@@ -587,8 +587,11 @@ struct BehzDev {
 #else
 #define BEHZ_OCC
 #endif
+#ifndef HPS_S60
+#define HPS_S60 1  // HPS's conversions on the in-place 31-bit column sums (hps_sp60)
+#endif
 #ifndef BEHZ_FENCES
-#define BEHZ_FENCES 1
+#define BEHZ_FENCES 9
 #endif
 // a scheduling fence per target of the BEHZ kernels: left free, the scheduler
 // hoists every target's uniform constants (hx / hf, h_b_q: up to 136 words,
@@ -597,7 +600,9 @@ struct BehzDev {
 // VALU instructions and runs at 36 VGPRs (8 waves): 650 -> 555 us per C3 call.
 // The floor's fences (bits 2, 4) remove its 104 SGPR spills too but cost 2% of
 // C3 (its Bsk loads can no longer run ahead of the previous target's products,
-// also with a one-ahead prefetch): profiles/r06/ab_behz_fences.txt
+// also with a one-ahead prefetch): profiles/r06/ab_behz_fences.txt.  The HPS
+// extension on column sums (bit 8): 86 -> 36 VGPRs, +0.4..0.9% on HPS C3
+// (profiles/r06/ab_hps_sp60.txt)
 // BEHZ_FENCES bits: 1 the extension's targets, 2 the floor's Bsk targets, 4 the floor's Q targets,
 // 8 the HPS extension's targets
 #define BEHZ_FENCE(bit)                                          \
@@ -924,7 +929,7 @@ __device__ __forceinline__ double hps_fsum(const u64 (&y)[NL], const double *w, 
 // Q -> P, the exact extension of the centred lift: y_i = [x_i (Q/q_i)^-1],
 // v = floor(0.5 + sum y_i / q_i), x mod p_j = sum_i y_i [Q/q_i]_{p_j} - v [Q]_{p_j}.
 // Layout as behz_extend_kernel (xb [2][n][2][nB][N]).
-template <int NL, bool SP, bool EX>
+template <int NL, bool SP, bool EX, bool S60 = false>
 __global__ void __launch_bounds__(EW_BLOCK) hps_extend_kernel(const u64 *__restrict__ a, const u64 *__restrict__ b,
                                                               u64 *__restrict__ xb, const HpsDev *hp,
                                                               const ModInfo *mods, u32 log_n, u32 n_items) {
@@ -950,7 +955,7 @@ __global__ void __launch_bounds__(EW_BLOCK) hps_extend_kernel(const u64 *__restr
     BEHZ_FENCE(8);
     if (EX || j < (int)nB) {
       const ModInfo m = mods[hp->bsk0 + j];
-      const u64 x = dot_mont<NL, SP>(y, &hp->qstar_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 x = behz_dot<NL, SP, S60>(y, &hp->qstar_R[0][j], BEHZ_MAXL + 1, L, m);
       const u64 vq = csub63(mont_mul<SP>(v, hp->Q_R[j], m), m.q);
       d[j * N] = sub_mod(x, vq, m.q);
     }
@@ -963,7 +968,7 @@ __global__ void __launch_bounds__(EW_BLOCK) hps_extend_kernel(const u64 *__restr
 // then y_j = [z_j (P/p_j)^-1], v = floor(0.5 + sum y_j / p_j) and
 // out_i = sum_j y_j [P/p_j]_{q_i} - v [P]_{q_i}.  Outputs as behz_floor_kernel
 // (r0, r1 -> out01; r2 -> dc and its own-digit ext slot times R).
-template <int NL, bool SP, bool EX>
+template <int NL, bool SP, bool EX, bool S60 = false>
 __global__ void __launch_bounds__(EW_BLOCK) hps_scale_kernel(const u64 *__restrict__ eq, const u64 *__restrict__ eb,
                                                              u64 *__restrict__ out01, u64 *__restrict__ dc,
                                                              u64 *__restrict__ ext, const HpsDev *hp,
@@ -992,7 +997,7 @@ __global__ void __launch_bounds__(EW_BLOCK) hps_scale_kernel(const u64 *__restri
     y[j] = 0;
     if (EX || j < (int)nB) {
       const ModInfo m = mods[hp->bsk0 + j];
-      const u64 zi = dot_mont<NL, SP>(x, &hp->I_R[0][j], BEHZ_MAXL + 1, L, m);
+      const u64 zi = behz_dot<NL, SP, S60>(x, &hp->I_R[0][j], BEHZ_MAXL + 1, L, m);
       const u64 zp = csub63(mont_mul<SP>(ld_nt(xb + j * N), hp->lam_R[j], m), m.q);
       const u64 zj = add_mod(add_mod(zi, zp, m.q), reduce128<SP>(U128{r, 0}, m), m.q);
       y[j] = csub63(mont_mul<SP>(zj, hp->pt_R[j], m), m.q);
@@ -1002,7 +1007,7 @@ __global__ void __launch_bounds__(EW_BLOCK) hps_scale_kernel(const u64 *__restri
   u64 *o = (p < 2) ? out01 + ((size_t)(ct * 2 + p) * L) * N + k : dc + ((size_t)ct * L) * N + k;
   for (int i = 0; i < (EX ? NL : (int)L); ++i) {
     const ModInfo m = mods[i];
-    const u64 cq = dot_mont<NL + 1, SP>(y, &hp->pstar_R[0][i], BEHZ_MAXL, nB, m);
+    const u64 cq = behz_dot<NL + 1, SP, S60>(y, &hp->pstar_R[0][i], BEHZ_MAXL, nB, m);
     const u64 vp = csub63(mont_mul<SP>(v, hp->P_R[i], m), m.q);
     const u64 res = sub_mod(cq, vp, m.q);
     o[i * N] = p == 2 && dsc ? csub63(mont_mul<SP>(res, dsc[i], m), m.q) : res;
@@ -1127,6 +1132,15 @@ static bool behz_q60(const fhe_ctx *c) {
     if (c->moduli[i] >= (1ull << 60)) return false;
   return true;
 }
+// HPS's conversions on the in-place column sums (dot_sp60_canon): Q below 2^60
+// (Q -> Bsk: the sources; Bsk -> Q: the targets and their constants) and every
+// Bsk modulus below 2^61 (the sp60 reduction's bound on the modulus)
+static bool hps_sp60(const fhe_ctx *c) {
+  if (!HPS_S60 || !behz_q60(c)) return false;
+  for (u32 j = 0; j < c->nB; ++j)
+    if (c->moduli[c->L + c->K + j] >= (1ull << 61)) return false;
+  return true;
+}
 
 template <bool SP>
 int behz_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
@@ -1168,7 +1182,8 @@ template <bool SP>
 int hps_extend_impl(fhe_ctx *c, const u64 *a, const u64 *b, u64 *xb, u32 n) {
   dim3 grid(c->n / EW_BLOCK, 4 * n);
   const HpsDev *hp = (const HpsDev *)c->hps;
-  if (c->L == 8) hipLaunchKernelGGL((hps_extend_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
+  if (c->L == 8 && hps_sp60(c)) hipLaunchKernelGGL((hps_extend_kernel<8, SP, true, true>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
+  else if (c->L == 8) hipLaunchKernelGGL((hps_extend_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
   else if (c->L <= 8) hipLaunchKernelGGL((hps_extend_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
   else if (c->L <= 16) hipLaunchKernelGGL((hps_extend_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
   else hipLaunchKernelGGL((hps_extend_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, a, b, xb, hp, c->d_mods, c->log_n, n);
@@ -1181,7 +1196,8 @@ int hps_scale_impl(fhe_ctx *c, const u64 *eq, const u64 *eb, u64 *out01, u64 *dc
   dim3 grid(c->n / EW_BLOCK, n * 3);
   const HpsDev *hp = (const HpsDev *)c->hps;
   const u32 QP = c->L + c->K;
-  if (c->L == 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  if (c->L == 8 && hps_sp60(c)) hipLaunchKernelGGL((hps_scale_kernel<8, SP, true, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
+  else if (c->L == 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, true>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
   else if (c->L <= 8) hipLaunchKernelGGL((hps_scale_kernel<8, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
   else if (c->L <= 16) hipLaunchKernelGGL((hps_scale_kernel<16, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
   else hipLaunchKernelGGL((hps_scale_kernel<24, SP, false>), grid, dim3(EW_BLOCK), 0, c->stream, eq, eb, out01, dc, ext, hp, c->d_mods, c->log_n, QP, c->alpha, ndig, dsc);
